@@ -1,0 +1,123 @@
+#!/usr/bin/env python
+"""Headline benchmark: CANNet training throughput (imgs/sec, whole node).
+
+Config (BASELINE.json): CANNet, ShanghaiTech-shape synthetic 768x1024 (HxW)
+crowd images, per-GPU batch 8 (weak scaling: global batch = 8*N), bf16
+compute with fp32 master weights, MSE(sum) loss, SGD momentum 0.95,
+lr 1e-7*world (train.py:25,63 of the reference), data-parallel over RCCL.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
+it is launched by torch.distributed.run (one rank per GPU).  W untimed steps,
+then exactly K timed steps bracketed by barrier + synchronize; the max over
+ranks is reported; rank 0 prints ONE JSON line.
+
+Every timed step is a full training step: H2D-free synthetic batch already
+resident (data="synthetic"), forward, loss, backward, gradient all-reduce,
+optimizer step.  ``--impl torch`` measures the stock PyTorch-ROCm reference
+stack (MIOpen convs + torch DDP) on the same config for comparison.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+BASELINE_IMGS_PER_SEC = None  # the reference publishes no throughput
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=8, help="per-GPU batch")
+    p.add_argument("--height", type=int, default=768)
+    p.add_argument("--width", type=int, default=1024)
+    p.add_argument("--impl", choices=["hip", "torch"], default=os.environ.get("CANNET_BENCH_IMPL", "hip"))
+    p.add_argument("--dtype", choices=["bf16", "fp32", "fp16"], default="bf16")
+    p.add_argument("--graph", type=int, default=1, help="hipGraph-capture the step (hip impl)")
+    p.add_argument("--profile-steps", type=int, default=0)
+    return p.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus != world and world > 1 and rank == 0:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from can_distributed_pytorch_amd.engine.trainer import build_trainer
+    from can_distributed_pytorch_amd.data.synthetic import make_synthetic_batch, expected_flops_per_image
+
+    torch.manual_seed(0)
+    trainer = build_trainer(impl=a.impl, dtype=a.dtype, device=dev, world=world, lr=1e-7,
+                            batch=a.batch, height=a.height, width=a.width, graph=bool(a.graph))
+    # a small pool of distinct synthetic batches, resident on the GPU
+    pool = [make_synthetic_batch(a.batch, a.height, a.width, seed=1000 * rank + i, device=dev) for i in range(2)]
+
+    def sync_all():
+        if world > 1:
+            dist.barrier(device_ids=[local])
+        torch.cuda.synchronize()
+
+    for i in range(a.warmup):
+        trainer.step(*pool[i % len(pool)])
+    sync_all()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        trainer.step(*pool[i % len(pool)])
+    sync_all()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    loss = trainer.last_loss()
+    ms = 1000.0 * dt / a.steps
+    imgs = a.batch * world * a.steps / dt
+    tflops = 3.0 * expected_flops_per_image(a.height, a.width) * imgs / 1e12
+    if rank == 0:
+        out = {
+            "metric": "imgs/sec (whole node) + ShanghaiTech-A MAE, CANNet at 1/2/4/8 MI355X",
+            "value": round(imgs, 3),
+            "unit": "imgs/sec",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (round(imgs / BASELINE_IMGS_PER_SEC, 4) if BASELINE_IMGS_PER_SEC else None),
+            "dtype": a.dtype,
+            "data": "synthetic (random-init weights, synthetic 768x1024 crowd images + count-preserving 1/8 density maps)",
+            "config": {"model": "CANNet", "global_batch": a.batch * world, "per_gpu_batch": a.batch,
+                       "image_hw": [a.height, a.width], "seq_len": None,
+                       "parallelism": f"dp{world}", "impl": a.impl,
+                       "graph": bool(a.graph) and a.impl == "hip",
+                       "optimizer": "SGD(m=0.95) fp32 master", "loss": "MSE(sum)"},
+            "train_tflops_per_s": round(tflops, 2),
+            "final_loss": loss,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier(device_ids=[local])
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

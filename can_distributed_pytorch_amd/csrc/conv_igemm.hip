@@ -1,0 +1,307 @@
+// MFMA implicit-GEMM convolution for gfx950 (forward and data-gradient).
+//
+// Replaces the cuDNN/MIOpen convolutions the reference gets implicitly from
+// nn.Conv2d (model/CANNet.py:14-17,114-115): 3x3 dilation 1 (VGG frontend),
+// 3x3 dilation 2 (backend), 1x1 (context module / head).  SURVEY §2.5 F1-B6.
+//
+// GEMM view (NHWC activations, K-contiguous packed weights):
+//   Y[m][co] = sum_k  Wp[co][k] * Xcol[m][k],   k = tap*Cin + ci,
+//   m = flattened output pixel (n, oh, ow), Xcol gathered on the fly with
+//   zero padding (no im2col buffer).
+// The data gradient is the same GEMM with the flipped/transposed weight pack
+// (Wd[ci][tap'][co] = W[co][8-tap'][ci]) applied to dY, so one kernel serves
+// both; the epilogue multiplies by the ReLU mask of the previous layer.
+//
+// CDNA4 mapping:
+//   * wave64, MFMA v_mfma_f32_16x16x32_bf16, fp32 accumulation;
+//   * each wave owns a 64(ch) x 64(pix) tile = 4x4 MFMA tiles (64 acc VGPRs);
+//     the weight tile is the MFMA A operand (rows = channels), the pixel tile
+//     the B operand (cols = pixels).  Weight rows are loaded into LDS in a
+//     permuted order so that every lane ends up holding 16 CONSECUTIVE output
+//     channels of one pixel -> two 16-byte global stores per 16x16 tile with no
+//     LDS round trip in the epilogue;
+//   * LDS tiles are [rows][64 bf16] (128-B rows) with the 16-B chunk index
+//     XOR-swizzled by (row & 7): conflict-free for the ds_read_b128 lane
+//     groups of gfx950 (checked exhaustively for the fragment read pattern);
+//   * K loop in 64-deep steps, register-staged double buffer: the next tile's
+//     global loads are issued before the MFMAs of the current tile and written
+//     to the other LDS buffer after them (one barrier per K step);
+//   * 1-D grid with a bijective XCD-aware remap so that the channel tiles
+//     sharing one pixel tile (and its halo) run on the same XCD / L2.
+#include "common.h"
+
+namespace can {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+struct ConvArgs {
+  const bf16_t* x;     // NHWC [N][H][W][Cin] bf16 (FIRST: Cin = 4, channel 3 zero)
+  const bf16_t* w;     // packed [Cout][Ktot] bf16
+  const float* bias;   // [Cout] fp32 (EPI_BIAS*) or nullptr
+  const bf16_t* mask;  // [M][Cout] bf16, output multiplied by (mask > 0) (EPI_MASK)
+  bf16_t* y;           // [M][Cout] bf16
+  int N, H, W, Cin, Cout, ksize, dil, M;
+};
+
+enum { EPI_BIAS_RELU = 0, EPI_MASK = 1, EPI_NONE = 2, EPI_BIAS = 3 };
+enum { LOAD_GENERIC = 0, LOAD_FIRST = 1 };
+
+__device__ __forceinline__ int perm_row(int rho) {
+  // LDS weight row rho -> local output channel, so that lane q of the MFMA
+  // D layout (rows q*4+r of tile jt) owns channels q*16 + jt*4 + r.
+  const int rl = rho & 63;
+  return (rho & ~63) | (((rl >> 2) & 3) << 4) | ((rl >> 4) << 2) | (rl & 3);
+}
+
+__device__ __forceinline__ int swz(int row, int chunk) { return (chunk ^ (row & 7)); }
+
+template <int WC, int WP, int LOAD, int EPI>
+__global__ void __launch_bounds__(64 * WC * WP)
+conv_igemm_kernel(ConvArgs a) {
+  constexpr int NT = 64 * WC * WP;
+  constexpr int TC = 64 * WC;          // output channels per block
+  constexpr int TP = 64 * WP;          // output pixels per block
+  constexpr int NA = TC * 8 / NT;      // 16-B weight chunks per thread per stage
+  constexpr int NB = TP * 8 / NT;      // 16-B pixel chunks per thread per stage
+  static_assert(NA >= 1 && NB >= 1, "tile too small");
+
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint4* As = reinterpret_cast<uint4*>(smem);                 // [2][TC][8]
+  uint4* Bs = As + 2 * TC * 8;                                // [2][TP][8]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wc = wave % WC;
+  const int wp = wave / WC;
+
+  const int nct = a.Cout / TC;
+  const int npt = (a.M + TP - 1) / TP;
+  const int tile = xcd_remap(blockIdx.x, nct * npt);
+  const int ct = tile % nct;
+  const int pt = tile / nct;
+
+  const int Ktot = (LOAD == LOAD_FIRST) ? 64 : a.ksize * a.ksize * a.Cin;
+  const int cchunks = (LOAD == LOAD_FIRST) ? 1 : a.Cin / 64;
+  const int nk = (LOAD == LOAD_FIRST) ? 1 : a.ksize * a.ksize * cchunks;
+  const int HW = a.H * a.W;
+
+  // ---- per-thread fixed rows -------------------------------------------
+  const bf16_t* wrow[NA];
+  int achunk[NA], arow[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int id = tid + NT * i;
+    arow[i] = id >> 3;
+    achunk[i] = id & 7;
+    wrow[i] = a.w + (size_t)(ct * TC + perm_row(arow[i])) * Ktot + achunk[i] * 8;
+  }
+  int bm[NB], boh[NB], bow[NB], brow[NB], bchunk[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int id = tid + NT * i;
+    brow[i] = id >> 3;
+    bchunk[i] = id & 7;
+    const int m = pt * TP + brow[i];
+    bm[i] = m;
+    const int r = m % HW;
+    boh[i] = (m < a.M) ? r / a.W : -100000;   // invalid rows never pass the bounds test
+    bow[i] = r % a.W;
+  }
+
+  uint4 ra[NA], rb[NB];
+
+  auto load_stage = [&](int ks) {
+    int tap = 0, c0 = 0;
+    if (LOAD == LOAD_GENERIC) {
+      tap = ks / cchunks;
+      c0 = (ks - tap * cchunks) * 64;
+    }
+#pragma unroll
+    for (int i = 0; i < NA; ++i) ra[i] = *reinterpret_cast<const uint4*>(wrow[i] + ks * 64);
+    if (LOAD == LOAD_GENERIC) {
+      const int kh = (a.ksize == 3) ? tap / 3 : 1;
+      const int kw = (a.ksize == 3) ? tap - kh * 3 : 1;
+      const int dh = (kh - 1) * a.dil, dw = (kw - 1) * a.dil;
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int ih = boh[i] + dh, iw = bow[i] + dw;
+        const bool ok = (ih >= 0) && (ih < a.H) && (iw >= 0) && (iw < a.W);
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (ok) v = *reinterpret_cast<const uint4*>(a.x + (size_t)(bm[i] + dh * a.W + dw) * a.Cin + c0 + bchunk[i] * 8);
+        rb[i] = v;
+      }
+    } else {
+      // first layer: Cin = 4 (8 B per pixel); chunk j = taps 2j, 2j+1
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        uint2 lo = make_uint2(0, 0), hi = make_uint2(0, 0);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int tap = bchunk[i] * 2 + h;
+          if (tap < 9) {
+            const int dh = (tap / 3 - 1) * a.dil, dw = (tap % 3 - 1) * a.dil;
+            const int ih = boh[i] + dh, iw = bow[i] + dw;
+            if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) {
+              const uint2 v = *reinterpret_cast<const uint2*>(a.x + (size_t)(bm[i] + dh * a.W + dw) * 4);
+              if (h == 0) lo = v; else hi = v;
+            }
+          }
+        }
+        rb[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      }
+    }
+  };
+  auto store_stage = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) As[(buf * TC + arow[i]) * 8 + swz(arow[i], achunk[i])] = ra[i];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) Bs[(buf * TP + brow[i]) * 8 + swz(brow[i], bchunk[i])] = rb[i];
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_stage(0);
+  store_stage(0);
+  __syncthreads();
+
+  const int fr = lane & 15;
+  const int fq = lane >> 4;
+  for (int ks = 0; ks < nk; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nk) load_stage(ks + 1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = kk * 4 + fq;
+      bf16x8_t af[4], bfr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = wc * 64 + j * 16 + fr;
+        af[j] = __builtin_bit_cast(bf16x8_t, As[(buf * TC + row) * 8 + swz(row, chunk)]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = wp * 64 + i * 16 + fr;
+        bfr[i] = __builtin_bit_cast(bf16x8_t, Bs[(buf * TP + row) * 8 + swz(row, chunk)]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], bfr[i], acc[j][i], 0, 0, 0);
+    }
+    if (ks + 1 < nk) store_stage(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane owns channels [chb, chb+16) of one pixel per tile i
+  const int chb = ct * TC + wc * 64 + fq * 16;
+  float bias[16];
+  if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS) {
+#pragma unroll
+    for (int c = 0; c < 16; c += 4) {
+      const float4 b4 = *reinterpret_cast<const float4*>(a.bias + chb + c);
+      bias[c] = b4.x; bias[c + 1] = b4.y; bias[c + 2] = b4.z; bias[c + 3] = b4.w;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = pt * TP + wp * 64 + i * 16 + fr;
+    if (m >= a.M) continue;
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[j * 4 + r] = acc[j][i][r];
+    if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        v[c] += bias[c];
+        if (EPI == EPI_BIAS_RELU) v[c] = fmaxf(v[c], 0.f);
+      }
+    }
+    const size_t off = (size_t)m * a.Cout + chb;
+    if (EPI == EPI_MASK) {
+      const uint4 m0 = *reinterpret_cast<const uint4*>(a.mask + off);
+      const uint4 m1 = *reinterpret_cast<const uint4*>(a.mask + off + 8);
+      const unsigned mw[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const unsigned short bits = (unsigned short)(mw[c >> 1] >> ((c & 1) * 16));
+        const bool pos = ((bits & 0x8000u) == 0) && ((bits & 0x7fffu) != 0);
+        v[c] = pos ? v[c] : 0.f;
+      }
+    }
+    uint4 o0 = make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
+    uint4 o1 = make_uint4(pack2bf(v[8], v[9]), pack2bf(v[10], v[11]), pack2bf(v[12], v[13]), pack2bf(v[14], v[15]));
+    *reinterpret_cast<uint4*>(a.y + off) = o0;
+    *reinterpret_cast<uint4*>(a.y + off + 8) = o1;
+  }
+}
+
+template <int WC, int WP, int LOAD, int EPI>
+static int launch_conv(const ConvArgs& a, hipStream_t s) {
+  constexpr int NT = 64 * WC * WP;
+  constexpr int TC = 64 * WC, TP = 64 * WP;
+  const size_t lds = 2 * (TC + TP) * 128;
+  auto kfn = conv_igemm_kernel<WC, WP, LOAD, EPI>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr_set = true;
+  }
+  const int nct = a.Cout / TC;
+  const int npt = (a.M + TP - 1) / TP;
+  hipLaunchKernelGGL(kfn, dim3(nct * npt), dim3(NT), lds, s, a);
+  return (int)hipGetLastError();
+}
+
+template <int LOAD, int EPI>
+static int dispatch_tiles(const ConvArgs& a, int tile_cfg, hipStream_t s) {
+  // tile_cfg: 0 = auto, 1 = 128ch x 128pix, 2 = 64ch x 256pix, 3 = 128ch x 256pix, 4 = 256ch x 128pix
+  int cfg = tile_cfg;
+  if (cfg == 0) {
+    if (a.Cout % 128 != 0) cfg = 2;
+    else if (a.Cout % 256 == 0 && a.M >= 65536) cfg = 4;
+    else cfg = 1;
+  }
+  switch (cfg) {
+    case 1: return launch_conv<2, 2, LOAD, EPI>(a, s);
+    case 2: return launch_conv<1, 4, LOAD, EPI>(a, s);
+    case 3: return launch_conv<2, 4, LOAD, EPI>(a, s);
+    case 4: return launch_conv<4, 2, LOAD, EPI>(a, s);
+  }
+  return -1;
+}
+
+}  // namespace can
+
+extern "C" int can_conv_igemm(const void* x, const void* w, const float* bias, const void* mask, void* y,
+                              int N, int H, int W, int Cin, int Cout, int ksize, int dil,
+                              int epi, int first, int tile_cfg, void* stream) {
+  using namespace can;
+  ConvArgs a;
+  a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.bias = bias; a.mask = (const bf16_t*)mask;
+  a.y = (bf16_t*)y; a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.ksize = ksize; a.dil = dil;
+  a.M = N * H * W;
+  if (Cout % 64 != 0) return -2;
+  if (!first && Cin % 64 != 0) return -3;
+  if (first && (Cin != 4 || ksize != 3)) return -4;
+  hipStream_t s = (hipStream_t)stream;
+#define CAN_EPI_CASE(L, E) \
+  if (epi == E) return dispatch_tiles<L, E>(a, tile_cfg, s);
+  if (first) {
+    CAN_EPI_CASE(LOAD_FIRST, EPI_BIAS_RELU)
+    return -5;
+  }
+  CAN_EPI_CASE(LOAD_GENERIC, EPI_BIAS_RELU)
+  CAN_EPI_CASE(LOAD_GENERIC, EPI_MASK)
+  CAN_EPI_CASE(LOAD_GENERIC, EPI_NONE)
+  CAN_EPI_CASE(LOAD_GENERIC, EPI_BIAS)
+#undef CAN_EPI_CASE
+  return -6;
+}

@@ -1,0 +1,77 @@
+"""Training-step engines shared by train.py and bench.py.
+
+Two implementations of ONE training step (zero_grad -> forward -> MSE(sum)
+-> backward + gradient all-reduce -> SGD(momentum 0.95)), the reference's
+step (utils/train_eval_utils.py:28-52):
+
+* ``TorchStepper`` — the stock PyTorch-ROCm reference stack: nn.Conv2d
+  (MIOpen), ATen elementwise, torch DDP (RCCL), torch.optim.SGD.  Used as the
+  "reference stack on MI355X" baseline and as the CPU/gloo path.
+* ``NativeStepper`` — this framework: the native executor (HIP MFMA kernels,
+  NHWC bf16, fused context module), the C++/RCCL bucketed reducer overlapped
+  with backward on a side stream, fused multi-tensor SGD over the flat fp32
+  master arena that also refreshes the bf16 packed weights, and (optionally)
+  the whole step captured once into a hipGraph and replayed.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from ..models.cannet import CANNet
+
+
+class TorchStepper:
+    def __init__(self, device, dtype="fp32", world=1, lr=1e-7, momentum=0.95, channels_last=None, model=None):
+        self.device = torch.device(device)
+        self.model = (model or CANNet(backend="torch")).to(self.device)
+        self.model.exec_backend = "torch"
+        self.dtype = dtype
+        self.channels_last = (dtype != "fp32") if channels_last is None else channels_last
+        if self.channels_last:
+            self.model = self.model.to(memory_format=torch.channels_last)
+        self.net = self.model
+        if world > 1:
+            dev_ids = [self.device.index] if self.device.type == "cuda" else None
+            self.net = torch.nn.parallel.DistributedDataParallel(self.model, device_ids=dev_ids)
+        self.opt = torch.optim.SGD([p for p in self.model.parameters() if p.requires_grad],
+                                   lr=lr * world, momentum=momentum, weight_decay=0)
+        self.crit = torch.nn.MSELoss(reduction="sum")
+        self._loss = None
+        self.autocast = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(dtype)
+        self.scaler = torch.amp.GradScaler("cuda") if dtype == "fp16" else None
+
+    def step(self, img, gt):
+        self.opt.zero_grad(set_to_none=True)
+        if self.channels_last:
+            img = img.contiguous(memory_format=torch.channels_last)
+        if self.autocast is not None:
+            with torch.autocast(self.device.type, dtype=self.autocast):
+                et = self.net(img)
+            loss = self.crit(et.float(), gt)
+        else:
+            et = self.net(img)
+            loss = self.crit(et, gt)
+        if self.scaler is not None:
+            self.scaler.scale(loss).backward()
+            self.scaler.step(self.opt)
+            self.scaler.update()
+        else:
+            loss.backward()
+            self.opt.step()
+        self._loss = loss.detach()
+        return self._loss
+
+    def last_loss(self) -> Optional[float]:
+        return None if self._loss is None else float(self._loss)
+
+
+def build_trainer(impl="hip", dtype="bf16", device="cuda", world=1, lr=1e-7, batch=8,
+                  height=768, width=1024, graph=True, model=None):
+    if impl == "torch":
+        return TorchStepper(device, dtype=dtype, world=world, lr=lr, model=model)
+    from .native import NativeStepper
+    return NativeStepper(device, dtype=dtype, world=world, lr=lr, batch=batch, height=height,
+                         width=width, graph=graph, model=model)

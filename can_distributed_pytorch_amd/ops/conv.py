@@ -1,0 +1,105 @@
+"""Python front-end of the gfx950 implicit-GEMM convolution kernels.
+
+Replaces the nn.Conv2d calls of the reference (model/CANNet.py:14-17,114-115)
+with NHWC bf16 MFMA kernels (csrc/conv_igemm.hip forward + data-gradient,
+csrc/conv_wgrad.hip weight-gradient).  All shape / dtype / layout checks are
+done here, on the host, before anything is launched.
+
+Weight layouts (packed from the fp32 master weights [Co][Ci][kh][kw]):
+  * forward  : [Co][kh][kw][Ci] bf16   (K = 9*Ci contiguous per output channel)
+  * dgrad    : [Ci][kh'][kw'][Co] bf16 with kh' = 2-kh, kw' = 2-kw (flipped)
+  * first    : [64][64] bf16, k = tap*4 + c (c < 3), zero padded (Cin=3 layer)
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _ext
+
+EPI_BIAS_RELU, EPI_MASK, EPI_NONE, EPI_BIAS = 0, 1, 2, 3
+BF16 = torch.bfloat16
+
+
+def pack_weight_fwd(w: torch.Tensor) -> torch.Tensor:
+    co = w.shape[0]
+    return w.detach().permute(0, 2, 3, 1).reshape(co, -1).to(BF16).contiguous()
+
+
+def pack_weight_dgrad(w: torch.Tensor) -> torch.Tensor:
+    ci = w.shape[1]
+    return w.detach().flip(2, 3).permute(1, 2, 3, 0).reshape(ci, -1).to(BF16).contiguous()
+
+
+def pack_weight_first(w: torch.Tensor) -> torch.Tensor:
+    co, ci, kh, kw = w.shape
+    assert ci == 3 and kh == 3 and kw == 3
+    wp = torch.zeros(co, 64, dtype=torch.float32, device=w.device)
+    wp[:, :36].view(co, 9, 4)[:, :, :3] = w.detach().float().permute(0, 2, 3, 1).reshape(co, 9, 3)
+    return wp.to(BF16).contiguous()
+
+
+def to_nhwc4(img: torch.Tensor) -> torch.Tensor:
+    """[N,3,H,W] float -> [N,H,W,4] bf16 (channel 3 = 0): the first layer's input layout."""
+    n, c, h, w = img.shape
+    assert c == 3
+    out = torch.zeros(n, h, w, 4, dtype=BF16, device=img.device)
+    out[..., :3] = img.permute(0, 2, 3, 1)
+    return out
+
+
+def _check_act(x: torch.Tensor, name: str, c: Optional[int] = None):
+    if not x.is_cuda:
+        raise ValueError(f"{name} must be a GPU tensor")
+    if x.dtype != BF16:
+        raise ValueError(f"{name} must be bf16, got {x.dtype}")
+    if not x.is_contiguous():
+        raise ValueError(f"{name} must be contiguous NHWC")
+    if c is not None and x.shape[-1] != c:
+        raise ValueError(f"{name} has {x.shape[-1]} channels, expected {c}")
+
+
+def conv_igemm(x: torch.Tensor, wpack: torch.Tensor, bias: Optional[torch.Tensor], *, ksize: int, dil: int = 1,
+               epi: int = EPI_BIAS_RELU, mask: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+               first: bool = False, tile: int = 0) -> torch.Tensor:
+    """y[N,H,W,Co] = epi(conv(x[N,H,W,Ci], W) ...), stride 1, 'same' padding = dil*(ksize//2)."""
+    C = _ext.require()
+    if x.dim() != 4:
+        raise ValueError("x must be [N,H,W,C]")
+    n, h, w, ci = x.shape
+    _check_act(x, "x")
+    co, k = wpack.shape
+    if wpack.dtype != BF16 or not wpack.is_contiguous():
+        raise ValueError("wpack must be contiguous bf16")
+    if first:
+        if ci != 4 or ksize != 3 or k != 64:
+            raise ValueError("first-layer conv expects x[...,4], 3x3, packed weight [Co,64]")
+    else:
+        if ci % 64 != 0:
+            raise ValueError(f"Cin={ci} must be a multiple of 64")
+        if k != ksize * ksize * ci:
+            raise ValueError(f"packed weight K={k} != {ksize}*{ksize}*{ci}")
+    if co % 64 != 0:
+        raise ValueError(f"Cout={co} must be a multiple of 64")
+    if ksize not in (1, 3):
+        raise ValueError("ksize must be 1 or 3")
+    if epi in (EPI_BIAS_RELU, EPI_BIAS):
+        if bias is None or bias.dtype != torch.float32 or bias.numel() != co or not bias.is_contiguous():
+            raise ValueError("bias must be contiguous fp32 [Cout]")
+    if epi == EPI_MASK:
+        if mask is None or tuple(mask.shape) != (n, h, w, co):
+            raise ValueError("mask must be [N,H,W,Cout]")
+        _check_act(mask, "mask")
+    if out is None:
+        out = torch.empty(n, h, w, co, dtype=BF16, device=x.device)
+    else:
+        if tuple(out.shape) != (n, h, w, co):
+            raise ValueError("out has the wrong shape")
+        _check_act(out, "out")
+    if n * h * w >= 2 ** 31 // max(ci, co):
+        raise ValueError("tensor too large for 32-bit pixel indexing")
+    C.conv_igemm(x.data_ptr(), wpack.data_ptr(), bias.data_ptr() if bias is not None else 0,
+                 mask.data_ptr() if mask is not None else 0, out.data_ptr(), n, h, w, ci, co, ksize, dil,
+                 epi, int(first), tile, _ext.stream_ptr(x.device))
+    return out
