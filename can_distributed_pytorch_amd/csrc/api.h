@@ -9,6 +9,33 @@ extern "C" {
 int can_conv_igemm(const void* x, const void* w, const float* bias, const void* mask, void* y, int N, int H, int W,
                    int Cin, int Cout, int ksize, int dil, int epi, int first, int tile_cfg, void* stream);
 
+int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, int target_blocks, int* S_out, int* mslice_out,
+                   int* cfg_out);
+int can_conv_wgrad(const void* dy, const void* x, float* ws, float* wsb, float* dw, float* db, int N, int H, int W,
+                   int Cin, int Cout, int ksize, int dil, int first, int S, int mslice, int cfg, float beta,
+                   float scale, void* stream);
+
+// elementwise.hip
+int can_maxpool_fwd(const void* x, void* y, int N, int H, int W, int C, void* stream);
+int can_maxpool_bwd_relu(const void* x, const void* dy, void* dx, int N, int H, int W, int C, void* stream);
+int can_head_fwd(const void* y, const float* w, const float* b, float* et, int P, void* stream);
+int can_head_train(const void* y, const float* w, const float* b, const float* gt, float* et, void* dy, float* part,
+                   int nblk, float* dw, float* db, float* loss, int P, float gscale, float beta, void* stream);
+int can_sgd_momentum(float* p, float* buf, const float* g, size_t n, float lr, float momentum, float gscale,
+                     int first, const float* flags, void* stream);
+int can_pack_conv(const float* w, void* fwd, void* dgr, int Co, int Ci, int taps, int first, void* stream);
+int can_img_to_nhwc4(const float* img, void* out, int N, int H, int W, void* stream);
+
+// context.hip
+int can_ctx_reduce(int mode, const void* in0, const void* sdir, const void* dc, float* rowacc, float* cells, int N,
+                   int h, int w, int C, void* stream);
+int can_ctx_expand(const void* fv, const float* T, void* cs, int N, int h, int w, int C, void* stream);
+int can_ctx_fuse(const void* fv, const void* ws, const float* T, void* cat, int N, int h, int w, int C, void* stream);
+int can_ctx_bwd_e1(const void* dcat, const void* ws, const float* T, void* dz, void* sdir, int N, int h, int w, int C,
+                   void* stream);
+int can_ctx_bwd_final(const void* dcat, const void* dc, const float* dave, const void* fv, void* dfv, int N, int h,
+                      int w, int C, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -40,4 +40,68 @@ PYBIND11_MODULE(_C, m) {
                          tile_cfg, P(stream)),
           "conv_igemm");
   });
+
+  m.def("wgrad_plan", [](int M, int Cin, int Cout, int ksize, int first, int target_blocks) {
+    int S = 0, ms = 0, cfg = 0;
+    check(can_wgrad_plan(M, Cin, Cout, ksize, first, target_blocks, &S, &ms, &cfg), "wgrad_plan");
+    return py::make_tuple(S, ms, cfg);
+  });
+  m.def("conv_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t ws, uintptr_t wsb, uintptr_t dw, uintptr_t db, int N,
+                         int H, int W, int Cin, int Cout, int ksize, int dil, int first, int S, int mslice, int cfg,
+                         float beta, float scale, uintptr_t stream) {
+    check(can_conv_wgrad(P(dy), P(x), (float*)ws, (float*)wsb, (float*)dw, (float*)db, N, H, W, Cin, Cout, ksize, dil,
+                         first, S, mslice, cfg, beta, scale, P(stream)),
+          "conv_wgrad");
+  });
+
+  // ---- elementwise
+  m.def("maxpool_fwd", [](uintptr_t x, uintptr_t y, int N, int H, int W, int C, uintptr_t st) {
+    check(can_maxpool_fwd(P(x), P(y), N, H, W, C, P(st)), "maxpool_fwd");
+  });
+  m.def("maxpool_bwd_relu", [](uintptr_t x, uintptr_t dy, uintptr_t dx, int N, int H, int W, int C, uintptr_t st) {
+    check(can_maxpool_bwd_relu(P(x), P(dy), P(dx), N, H, W, C, P(st)), "maxpool_bwd_relu");
+  });
+  m.def("head_fwd", [](uintptr_t y, uintptr_t w, uintptr_t b, uintptr_t et, int Pn, uintptr_t st) {
+    check(can_head_fwd(P(y), (const float*)w, (const float*)b, (float*)et, Pn, P(st)), "head_fwd");
+  });
+  m.def("head_train", [](uintptr_t y, uintptr_t w, uintptr_t b, uintptr_t gt, uintptr_t et, uintptr_t dy,
+                         uintptr_t part, int nblk, uintptr_t dw, uintptr_t db, uintptr_t loss, int Pn, float gscale,
+                         float beta, uintptr_t st) {
+    check(can_head_train(P(y), (const float*)w, (const float*)b, (const float*)gt, (float*)et, P(dy), (float*)part,
+                         nblk, (float*)dw, (float*)db, (float*)loss, Pn, gscale, beta, P(st)),
+          "head_train");
+  });
+  m.def("sgd_momentum", [](uintptr_t p, uintptr_t buf, uintptr_t g, size_t n, float lr, float mom, float gscale,
+                           int first, uintptr_t flags, uintptr_t st) {
+    check(can_sgd_momentum((float*)p, (float*)buf, (const float*)g, n, lr, mom, gscale, first, (const float*)flags,
+                           P(st)),
+          "sgd_momentum");
+  });
+  m.def("pack_conv", [](uintptr_t w, uintptr_t fwd, uintptr_t dgr, int Co, int Ci, int taps, int first, uintptr_t st) {
+    check(can_pack_conv((const float*)w, P(fwd), P(dgr), Co, Ci, taps, first, P(st)), "pack_conv");
+  });
+  m.def("img_to_nhwc4", [](uintptr_t img, uintptr_t out, int N, int H, int W, uintptr_t st) {
+    check(can_img_to_nhwc4((const float*)img, P(out), N, H, W, P(st)), "img_to_nhwc4");
+  });
+  // ---- context module
+  m.def("ctx_reduce", [](int mode, uintptr_t in0, uintptr_t sdir, uintptr_t dc, uintptr_t rowacc, uintptr_t cells,
+                         int N, int h, int w, int C, uintptr_t st) {
+    check(can_ctx_reduce(mode, P(in0), P(sdir), P(dc), (float*)rowacc, (float*)cells, N, h, w, C, P(st)),
+          "ctx_reduce");
+  });
+  m.def("ctx_expand", [](uintptr_t fv, uintptr_t T, uintptr_t cs, int N, int h, int w, int C, uintptr_t st) {
+    check(can_ctx_expand(P(fv), (const float*)T, P(cs), N, h, w, C, P(st)), "ctx_expand");
+  });
+  m.def("ctx_fuse", [](uintptr_t fv, uintptr_t ws, uintptr_t T, uintptr_t cat, int N, int h, int w, int C,
+                       uintptr_t st) {
+    check(can_ctx_fuse(P(fv), P(ws), (const float*)T, P(cat), N, h, w, C, P(st)), "ctx_fuse");
+  });
+  m.def("ctx_bwd_e1", [](uintptr_t dcat, uintptr_t ws, uintptr_t T, uintptr_t dz, uintptr_t sdir, int N, int h, int w,
+                         int C, uintptr_t st) {
+    check(can_ctx_bwd_e1(P(dcat), P(ws), (const float*)T, P(dz), P(sdir), N, h, w, C, P(st)), "ctx_bwd_e1");
+  });
+  m.def("ctx_bwd_final", [](uintptr_t dcat, uintptr_t dc, uintptr_t dave, uintptr_t fv, uintptr_t dfv, int N, int h,
+                            int w, int C, uintptr_t st) {
+    check(can_ctx_bwd_final(P(dcat), P(dc), (const float*)dave, P(fv), P(dfv), N, h, w, C, P(st)), "ctx_bwd_final");
+  });
 }

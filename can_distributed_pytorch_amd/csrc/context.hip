@@ -1,0 +1,397 @@
+// Multi-scale context module of CANNet (model/CANNet.py:42-87), gfx950.
+//
+// Forward, per scale S in {1,2,3,6}:
+//   ave_S = adaptive_avg_pool(fv, S)       -> ctx_rows(POOL) + ctx_cells(POOL)
+//   A_S   = conv{S}_1(ave_S)               -> tiny [N*S*S,512]x[512,512] GEMM (host side)
+//   s_S   = bilinear_up(A_S, align_corners)  (never materialised: recomputed
+//                                            from the 50-cell table on the fly)
+//   c_S   = s_S - fv                       -> ctx_expand (all 4 scales, one read of fv)
+//   w_S   = sigmoid(conv{S}_2(c_S))        -> MFMA GEMM with sigmoid epilogue (conv_igemm)
+//   fi    = sum w_S s_S / (sum w_S + 1e-12); out = cat(fv, fi)   -> ctx_fuse
+// Backward:
+//   ctx_bwd_e1  : dz_S = dfi (s_S - fi)/D * w_S(1-w_S),  sdir_S = dfi w_S / D
+//   (host)      : dc_S = dz_S W_S2 (MFMA), dW_S2 = dz_S^T c_S (MFMA wgrad)
+//   ctx_rows(BILINEAR) + ctx_cells(BILINEAR): dA_S = upsample^T (sdir_S + dc_S)
+//   (host)      : dW_S1 = dA_S^T ave_S, dave_S = dA_S W_S1
+//   ctx_bwd_final: dfv = (dcat_fv - sum dc_S + sum pool^T dave_S) * (fv > 0)
+//
+// The 50 cells of the four scales share one table layout [N][50][C]
+// (cell offsets 0, 1, 5, 14); the 12 column bins of the separable row pass
+// share [N][h][12][C] (bin offsets 0, 1, 3, 6).  All reductions are
+// fixed-order (deterministic, no atomics).  Adaptive-pool bins follow ATen:
+// start = floor(i*L/S), end = ceil((i+1)*L/S) (overlapping when L % S != 0).
+#include "common.h"
+
+namespace can {
+
+__constant__ int kScale[4] = {1, 2, 3, 6};
+__constant__ int kCellOff[4] = {0, 1, 5, 14};
+__constant__ int kBinOff[4] = {0, 1, 3, 6};
+
+__device__ __forceinline__ void unpack8c(const uint4& v, float* f) {
+  const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ uint4 pack8c(const float* f) {
+  return make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
+}
+
+// adaptive-avg-pool bin [start,end) of index i at scale S over length L
+__device__ __forceinline__ void pool_bin(int i, int S, int L, int& st, int& en) {
+  st = (i * L) / S;
+  en = ((i + 1) * L + S - 1) / S;
+}
+// weight of bin/cell j (scale S) for position x over length L
+template <bool POOL>
+__device__ __forceinline__ float axis_w(int j, int S, int x, int L) {
+  if (POOL) {
+    int st, en;
+    pool_bin(j, S, L, st, en);
+    return (x >= st && x < en) ? 1.f / (float)(en - st) : 0.f;
+  } else {
+    const float scale = (L > 1) ? (float)(S - 1) / (float)(L - 1) : 0.f;
+    const float src = scale * (float)x;
+    const int x0 = (int)src;
+    const int x1 = x0 + ((x0 < S - 1) ? 1 : 0);
+    const float lam = src - (float)x0;
+    float wv = 0.f;
+    if (j == x0) wv += 1.f - lam;
+    if (j == x1) wv += lam;
+    return wv;
+  }
+}
+// bilinear taps of position x (align_corners=True)
+__device__ __forceinline__ void bil(int S, int x, int L, int& x0, int& x1, float& lam) {
+  const float scale = (L > 1) ? (float)(S - 1) / (float)(L - 1) : 0.f;
+  const float src = scale * (float)x;
+  x0 = (int)src;
+  x1 = x0 + ((x0 < S - 1) ? 1 : 0);
+  lam = src - (float)x0;
+}
+
+// ------------------------------------------------------------- row pass
+// rowacc[n][y][bin][c] = sum_x wx(bin, x) * in_S(bin)[n][y][x][c]
+// POOL: one input (fv) for all scales.  BILINEAR: per scale the sum of two
+// inputs (sdir_S + dc_S), in[2*S_idx] and in[2*S_idx+1], each [P][C].
+template <bool POOL>
+__global__ void __launch_bounds__(256) ctx_rows_kernel(const uint4* __restrict__ in0, const uint4* __restrict__ sdir,
+                                                       const uint4* __restrict__ dc, float* __restrict__ rowacc,
+                                                       int N, int h, int w, int C) {
+  const int C8 = C >> 3;
+  const size_t P = (size_t)N * h * w;
+  const size_t total = (size_t)N * h * C8;   // one thread per (n, y, 8-channel group)
+  for (size_t t = blockIdx.x * 256 + threadIdx.x; t < total; t += (size_t)gridDim.x * 256) {
+    const int cg = t % C8;
+    const size_t ny = t / C8;                 // n*h + y
+    float acc[12][8];
+#pragma unroll
+    for (int b = 0; b < 12; ++b)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[b][k] = 0.f;
+    for (int x = 0; x < w; ++x) {
+      const size_t pix = ny * w + x;
+      if (POOL) {
+        float v[8];
+        unpack8c(in0[pix * C8 + cg], v);
+#pragma unroll
+        for (int si = 0; si < 4; ++si) {
+          const int S = (si == 0) ? 1 : (si == 1) ? 2 : (si == 2) ? 3 : 6;
+          const int bo = (si == 0) ? 0 : (si == 1) ? 1 : (si == 2) ? 3 : 6;
+#pragma unroll
+          for (int j = 0; j < 6; ++j) {
+            if (j < S) {
+              const float wt = axis_w<true>(j, S, x, w);
+#pragma unroll
+              for (int k = 0; k < 8; ++k) acc[bo + j][k] += wt * v[k];
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int si = 0; si < 4; ++si) {
+          const int S = (si == 0) ? 1 : (si == 1) ? 2 : (si == 2) ? 3 : 6;
+          const int bo = (si == 0) ? 0 : (si == 1) ? 1 : (si == 2) ? 3 : 6;
+          float v[8], u[8];
+          unpack8c(sdir[(size_t)si * P * C8 + pix * C8 + cg], v);
+          unpack8c(dc[(size_t)si * P * C8 + pix * C8 + cg], u);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] += u[k];
+#pragma unroll
+          for (int j = 0; j < 6; ++j) {
+            if (j < S) {
+              const float wt = axis_w<false>(j, S, x, w);
+#pragma unroll
+              for (int k = 0; k < 8; ++k) acc[bo + j][k] += wt * v[k];
+            }
+          }
+        }
+      }
+    }
+    float* o = rowacc + (ny * 12) * C + cg * 8;
+#pragma unroll
+    for (int b = 0; b < 12; ++b) {
+      *reinterpret_cast<float4*>(o + (size_t)b * C) = make_float4(acc[b][0], acc[b][1], acc[b][2], acc[b][3]);
+      *reinterpret_cast<float4*>(o + (size_t)b * C + 4) = make_float4(acc[b][4], acc[b][5], acc[b][6], acc[b][7]);
+    }
+  }
+}
+
+// ------------------------------------------------------------- cell pass
+// cells[n][cell(S,i,j)][c] = sum_y wy(i, y) * rowacc[n][y][bin(S,j)][c]
+template <bool POOL>
+__global__ void __launch_bounds__(256) ctx_cells_kernel(const float* __restrict__ rowacc, float* __restrict__ cells,
+                                                        int N, int h, int C) {
+  const size_t total = (size_t)N * 50 * C;
+  for (size_t t = blockIdx.x * 256 + threadIdx.x; t < total; t += (size_t)gridDim.x * 256) {
+    const int c = t % C;
+    const int cell = (t / C) % 50;
+    const int n = t / ((size_t)C * 50);
+    int si = (cell >= 14) ? 3 : (cell >= 5) ? 2 : (cell >= 1) ? 1 : 0;
+    const int S = kScale[si];
+    const int local = cell - kCellOff[si];
+    const int i = local / S, j = local % S;
+    const int bin = kBinOff[si] + j;
+    float s = 0.f;
+    for (int y = 0; y < h; ++y) {
+      const float wt = axis_w<POOL>(i, S, y, h);
+      if (wt != 0.f) s += wt * rowacc[(((size_t)n * h + y) * 12 + bin) * C + c];
+    }
+    cells[t] = s;
+  }
+}
+
+// value of the bilinear upsample of table T (cells of scale si) at (y, x), 8 channels
+__device__ __forceinline__ void up8(const float* __restrict__ T, int n, int si, int y, int x, int h, int w, int C,
+                                    int cg, float* out) {
+  const int S = kScale[si];
+  int y0, y1, x0, x1;
+  float ly, lx;
+  bil(S, y, h, y0, y1, ly);
+  bil(S, x, w, x0, x1, lx);
+  const float* base = T + ((size_t)n * 50 + kCellOff[si]) * C + cg * 8;
+  const float w00 = (1.f - ly) * (1.f - lx), w01 = (1.f - ly) * lx, w10 = ly * (1.f - lx), w11 = ly * lx;
+  const float* p00 = base + (size_t)(y0 * S + x0) * C;
+  const float* p01 = base + (size_t)(y0 * S + x1) * C;
+  const float* p10 = base + (size_t)(y1 * S + x0) * C;
+  const float* p11 = base + (size_t)(y1 * S + x1) * C;
+#pragma unroll
+  for (int k = 0; k < 8; k += 4) {
+    const float4 a = *reinterpret_cast<const float4*>(p00 + k), b = *reinterpret_cast<const float4*>(p01 + k);
+    const float4 c = *reinterpret_cast<const float4*>(p10 + k), d = *reinterpret_cast<const float4*>(p11 + k);
+    out[k + 0] = w00 * a.x + w01 * b.x + w10 * c.x + w11 * d.x;
+    out[k + 1] = w00 * a.y + w01 * b.y + w10 * c.y + w11 * d.y;
+    out[k + 2] = w00 * a.z + w01 * b.z + w10 * c.z + w11 * d.z;
+    out[k + 3] = w00 * a.w + w01 * b.w + w10 * c.w + w11 * d.w;
+  }
+}
+
+// c_S = up_S - fv for the 4 scales: cs[si][P][C] bf16
+__global__ void __launch_bounds__(256) ctx_expand_kernel(const uint4* __restrict__ fv, const float* __restrict__ T,
+                                                         uint4* __restrict__ cs, int N, int h, int w, int C) {
+  const int C8 = C >> 3;
+  const size_t P = (size_t)N * h * w;
+  const size_t total = P * C8;
+  for (size_t t = blockIdx.x * 256 + threadIdx.x; t < total; t += (size_t)gridDim.x * 256) {
+    const int cg = t % C8;
+    const size_t p = t / C8;
+    const int x = p % w;
+    const int y = (p / w) % h;
+    const int n = p / ((size_t)w * h);
+    float f[8];
+    unpack8c(fv[t], f);
+#pragma unroll
+    for (int si = 0; si < 4; ++si) {
+      float u[8];
+      up8(T, n, si, y, x, h, w, C, cg, u);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) u[k] -= f[k];
+      cs[(size_t)si * total + t] = pack8c(u);
+    }
+  }
+}
+
+// cat[p] = [fv | fi],  fi = sum w_S s_S / (sum w_S + 1e-12)
+__global__ void __launch_bounds__(256) ctx_fuse_kernel(const uint4* __restrict__ fv, const uint4* __restrict__ ws,
+                                                       const float* __restrict__ T, uint4* __restrict__ cat, int N,
+                                                       int h, int w, int C) {
+  const int C8 = C >> 3;
+  const size_t P = (size_t)N * h * w;
+  const size_t total = P * C8;
+  for (size_t t = blockIdx.x * 256 + threadIdx.x; t < total; t += (size_t)gridDim.x * 256) {
+    const int cg = t % C8;
+    const size_t p = t / C8;
+    const int x = p % w;
+    const int y = (p / w) % h;
+    const int n = p / ((size_t)w * h);
+    float num[8], den[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { num[k] = 0.f; den[k] = 0.f; }
+#pragma unroll
+    for (int si = 0; si < 4; ++si) {
+      float u[8], wv[8];
+      up8(T, n, si, y, x, h, w, C, cg, u);
+      unpack8c(ws[(size_t)si * total + t], wv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { num[k] += wv[k] * u[k]; den[k] += wv[k]; }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) num[k] = num[k] / (den[k] + 1e-12f);
+    cat[p * 2 * C8 + cg] = fv[t];
+    cat[p * 2 * C8 + C8 + cg] = pack8c(num);
+  }
+}
+
+// backward elementwise: dz_S and sdir_S for the 4 scales
+__global__ void __launch_bounds__(256) ctx_bwd_e1_kernel(const uint4* __restrict__ dcat, const uint4* __restrict__ ws,
+                                                         const float* __restrict__ T, uint4* __restrict__ dz,
+                                                         uint4* __restrict__ sdir, int N, int h, int w, int C) {
+  const int C8 = C >> 3;
+  const size_t P = (size_t)N * h * w;
+  const size_t total = P * C8;
+  for (size_t t = blockIdx.x * 256 + threadIdx.x; t < total; t += (size_t)gridDim.x * 256) {
+    const int cg = t % C8;
+    const size_t p = t / C8;
+    const int x = p % w;
+    const int y = (p / w) % h;
+    const int n = p / ((size_t)w * h);
+    float s[4][8], wv[4][8], num[8], den[8], dfi[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { num[k] = 0.f; den[k] = 0.f; }
+#pragma unroll
+    for (int si = 0; si < 4; ++si) {
+      up8(T, n, si, y, x, h, w, C, cg, s[si]);
+      unpack8c(ws[(size_t)si * total + t], wv[si]);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { num[k] += wv[si][k] * s[si][k]; den[k] += wv[si][k]; }
+    }
+    unpack8c(dcat[p * 2 * C8 + C8 + cg], dfi);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { den[k] += 1e-12f; num[k] = num[k] / den[k]; }   // num := fi
+#pragma unroll
+    for (int si = 0; si < 4; ++si) {
+      float a[8], b[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float g = dfi[k] / den[k];
+        const float dws = g * (s[si][k] - num[k]);
+        a[k] = dws * wv[si][k] * (1.f - wv[si][k]);
+        b[k] = g * wv[si][k];
+      }
+      dz[(size_t)si * total + t] = pack8c(a);
+      sdir[(size_t)si * total + t] = pack8c(b);
+    }
+  }
+}
+
+// dfv = (dcat_fv - sum_S dc_S + sum_S pool^T(dave_S)) * (fv > 0)
+__global__ void __launch_bounds__(256) ctx_bwd_final_kernel(const uint4* __restrict__ dcat,
+                                                            const uint4* __restrict__ dc, const float* __restrict__ dave,
+                                                            const uint4* __restrict__ fv, uint4* __restrict__ dfv,
+                                                            int N, int h, int w, int C) {
+  const int C8 = C >> 3;
+  const size_t P = (size_t)N * h * w;
+  const size_t total = P * C8;
+  for (size_t t = blockIdx.x * 256 + threadIdx.x; t < total; t += (size_t)gridDim.x * 256) {
+    const int cg = t % C8;
+    const size_t p = t / C8;
+    const int x = p % w;
+    const int y = (p / w) % h;
+    const int n = p / ((size_t)w * h);
+    float g[8], u[8];
+    unpack8c(dcat[p * 2 * C8 + cg], g);
+#pragma unroll
+    for (int si = 0; si < 4; ++si) {
+      unpack8c(dc[(size_t)si * total + t], u);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[k] -= u[k];
+      const int S = kScale[si];
+      // bins containing (y, x): at most 2 per axis
+      for (int i = 0; i < S; ++i) {
+        int ys, ye;
+        pool_bin(i, S, h, ys, ye);
+        if (y < ys || y >= ye) continue;
+        for (int j = 0; j < S; ++j) {
+          int xs, xe;
+          pool_bin(j, S, w, xs, xe);
+          if (x < xs || x >= xe) continue;
+          const float inv = 1.f / (float)((ye - ys) * (xe - xs));
+          const float* d = dave + ((size_t)n * 50 + kCellOff[si] + i * S + j) * C + cg * 8;
+          const float4 a = *reinterpret_cast<const float4*>(d), b = *reinterpret_cast<const float4*>(d + 4);
+          g[0] += a.x * inv; g[1] += a.y * inv; g[2] += a.z * inv; g[3] += a.w * inv;
+          g[4] += b.x * inv; g[5] += b.y * inv; g[6] += b.z * inv; g[7] += b.w * inv;
+        }
+      }
+    }
+    float f[8];
+    unpack8c(fv[t], f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g[k] = (f[k] > 0.f) ? g[k] : 0.f;
+    dfv[t] = pack8c(g);
+  }
+}
+
+static inline int gridn(size_t n, int cap = 8192) {
+  size_t g = (n + 255) / 256;
+  if (g > (size_t)cap) g = cap;
+  return g < 1 ? 1 : (int)g;
+}
+
+}  // namespace can
+
+using namespace can;
+
+// mode 0: POOL(fv -> ave cells); mode 1: BILINEAR^T(sdir+dc -> dA cells)
+extern "C" int can_ctx_reduce(int mode, const void* in0, const void* sdir, const void* dc, float* rowacc, float* cells,
+                              int N, int h, int w, int C, void* stream) {
+  if (C & 7) return -2;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t tr = (size_t)N * h * (C / 8);
+  if (mode == 0)
+    hipLaunchKernelGGL(ctx_rows_kernel<true>, dim3(gridn(tr)), dim3(256), 0, s, (const uint4*)in0, nullptr, nullptr,
+                       rowacc, N, h, w, C);
+  else
+    hipLaunchKernelGGL(ctx_rows_kernel<false>, dim3(gridn(tr)), dim3(256), 0, s, nullptr, (const uint4*)sdir,
+                       (const uint4*)dc, rowacc, N, h, w, C);
+  const size_t tc = (size_t)N * 50 * C;
+  if (mode == 0)
+    hipLaunchKernelGGL(ctx_cells_kernel<true>, dim3(gridn(tc)), dim3(256), 0, s, rowacc, cells, N, h, C);
+  else
+    hipLaunchKernelGGL(ctx_cells_kernel<false>, dim3(gridn(tc)), dim3(256), 0, s, rowacc, cells, N, h, C);
+  return (int)hipGetLastError();
+}
+
+extern "C" int can_ctx_expand(const void* fv, const float* T, void* cs, int N, int h, int w, int C, void* stream) {
+  if (C & 7) return -2;
+  hipLaunchKernelGGL(ctx_expand_kernel, dim3(gridn((size_t)N * h * w * (C / 8))), dim3(256), 0, (hipStream_t)stream,
+                     (const uint4*)fv, T, (uint4*)cs, N, h, w, C);
+  return (int)hipGetLastError();
+}
+
+extern "C" int can_ctx_fuse(const void* fv, const void* ws, const float* T, void* cat, int N, int h, int w, int C,
+                            void* stream) {
+  if (C & 7) return -2;
+  hipLaunchKernelGGL(ctx_fuse_kernel, dim3(gridn((size_t)N * h * w * (C / 8))), dim3(256), 0, (hipStream_t)stream,
+                     (const uint4*)fv, (const uint4*)ws, T, (uint4*)cat, N, h, w, C);
+  return (int)hipGetLastError();
+}
+
+extern "C" int can_ctx_bwd_e1(const void* dcat, const void* ws, const float* T, void* dz, void* sdir, int N, int h,
+                              int w, int C, void* stream) {
+  if (C & 7) return -2;
+  hipLaunchKernelGGL(ctx_bwd_e1_kernel, dim3(gridn((size_t)N * h * w * (C / 8))), dim3(256), 0, (hipStream_t)stream,
+                     (const uint4*)dcat, (const uint4*)ws, T, (uint4*)dz, (uint4*)sdir, N, h, w, C);
+  return (int)hipGetLastError();
+}
+
+extern "C" int can_ctx_bwd_final(const void* dcat, const void* dc, const float* dave, const void* fv, void* dfv,
+                                 int N, int h, int w, int C, void* stream) {
+  if (C & 7) return -2;
+  hipLaunchKernelGGL(ctx_bwd_final_kernel, dim3(gridn((size_t)N * h * w * (C / 8))), dim3(256), 0,
+                     (hipStream_t)stream, (const uint4*)dcat, (const uint4*)dc, dave, (const uint4*)fv, (uint4*)dfv, N,
+                     h, w, C);
+  return (int)hipGetLastError();
+}

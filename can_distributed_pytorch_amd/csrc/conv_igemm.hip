@@ -43,7 +43,7 @@ struct ConvArgs {
   int N, H, W, Cin, Cout, ksize, dil, M;
 };
 
-enum { EPI_BIAS_RELU = 0, EPI_MASK = 1, EPI_NONE = 2, EPI_BIAS = 3 };
+enum { EPI_BIAS_RELU = 0, EPI_MASK = 1, EPI_NONE = 2, EPI_BIAS = 3, EPI_SIGMOID = 4 };
 enum { LOAD_GENERIC = 0, LOAD_FIRST = 1 };
 
 __device__ __forceinline__ int perm_row(int rho) {
@@ -224,6 +224,10 @@ conv_igemm_kernel(ConvArgs a) {
         if (EPI == EPI_BIAS_RELU) v[c] = fmaxf(v[c], 0.f);
       }
     }
+    if (EPI == EPI_SIGMOID) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) v[c] = 1.f / (1.f + __expf(-v[c]));
+    }
     const size_t off = (size_t)m * a.Cout + chb;
     if (EPI == EPI_MASK) {
       const uint4 m0 = *reinterpret_cast<const uint4*>(a.mask + off);
@@ -302,6 +306,7 @@ extern "C" int can_conv_igemm(const void* x, const void* w, const float* bias, c
   CAN_EPI_CASE(LOAD_GENERIC, EPI_MASK)
   CAN_EPI_CASE(LOAD_GENERIC, EPI_NONE)
   CAN_EPI_CASE(LOAD_GENERIC, EPI_BIAS)
+  CAN_EPI_CASE(LOAD_GENERIC, EPI_SIGMOID)
 #undef CAN_EPI_CASE
   return -6;
 }

@@ -1,0 +1,383 @@
+// MFMA weight-gradient kernel for the NHWC implicit-GEMM convolutions (gfx950).
+//
+// Replaces cuDNN/MIOpen's backward-filter of every nn.Conv2d in the reference
+// (model/CANNet.py:14-25; SURVEY §2.5 "convolution_backward x25").
+//
+//   dW[co][k] = sum_m dY[m][co] * Xcol[m][k],   k = tap*Cin + ci
+//   db[co]    = sum_m dY[m][co]
+//
+// The reduction runs over output pixels m (up to N*H*W = 6.3M at batch 8,
+// 768x1024), i.e. along the OUTER (strided) dimension of both NHWC operands.
+// Both tiles are staged in LDS exactly as they sit in memory ([pixel][channel]
+// rows, coalesced 16-B loads, zero-filled outside the image) and the MFMA
+// fragments, which need 8 consecutive PIXELS per lane, are read with the
+// gfx950 hardware-transpose LDS read ds_read_b64_tr_b16 (2 reads per
+// fragment).  The 8-B chunk index of each LDS row is XOR-swizzled so that the
+// 32 addresses of each transposed read hit 32 distinct 8-B bank slots.
+//
+// Work split: block = (co tile, k tile, pixel slice).  Slices write fp32
+// partial slabs ws[slice][k][co] (4 consecutive co per lane -> 16-B stores);
+// wgrad_reduce sums the slabs in a fixed order (deterministic, no atomics)
+// and scatters the result into the PyTorch weight layout [co][ci][kh][kw] of
+// the flat fp32 gradient arena (optionally accumulating).  The bias gradient
+// rides along: blocks of k-tile 0 run one extra MFMA per co tile against a
+// ones operand.
+//
+// Wave layouts (4 waves / 256 threads):
+//   <2,2,1>: 128 co x 128 k tile, 64-pixel stages, each wave 64x64 x 2 k-steps
+//   <1,1,4>: 64 co x 64 k tile, 128-pixel stages, each wave a 32-pixel quarter
+//            of every stage; the 4 partial tiles are summed through LDS.
+#include "common.h"
+
+namespace can {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+struct WgradArgs {
+  const bf16_t* dy;   // [M][Cout]
+  const bf16_t* x;    // [N][H][W][Cin] (FIRST: Cin = 4)
+  float* ws;          // [S][Ktot][Cout] partial slabs
+  float* wsb;         // [S][Cout] bias partials (or nullptr)
+  int N, H, W, Cin, Cout, ksize, dil, M;
+  int Ktot, S, mslice;
+};
+
+// 8-byte-chunk swizzle of an LDS row (row bytes = 2*RW): see file header.
+template <int RW>
+__device__ __forceinline__ int swz8(int row, int c8) {
+  if (RW == 128) return c8 ^ (((row & 3) | (((row >> 3) & 1) << 2)) << 2);
+  else return c8 ^ (((((row >> 1) & 1)) | (((row >> 3) & 1) << 1)) << 2);
+}
+
+template <int WC, int WK, int WM, bool FIRST>
+__global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
+  constexpr int TCo = 64 * WC;
+  constexpr int TK = 64 * WK;
+  constexpr int KSUB = (WM == 1) ? 2 : 1;
+  constexpr int BKM = 32 * KSUB * WM;            // pixels per stage
+  constexpr int CA = TCo / 8, CB = TK / 8;        // 16-B chunks per row
+  constexpr int NA = BKM * CA / 256, NB = BKM * CB / 256;
+  static_assert(WC * WK * WM == 4, "4 waves");
+  static_assert(NA >= 1 && NB >= 1, "");
+
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem);            // [2][BKM][TCo]
+  bf16_t* Bs = As + 2 * BKM * TCo;                          // [2][BKM][TK]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wc = wave % WC, wk = (wave / WC) % WK, wm = wave / (WC * WK);
+
+  const int nco = a.Cout / TCo, nkt = a.Ktot / TK;
+  const int ntile = nco * nkt;
+  const int bid = xcd_remap(blockIdx.x, ntile * a.S);
+  const int tile = bid % ntile;                  // slices of one tile are spread, tiles adjacent
+  const int slice = bid / ntile;
+  const int cot = tile % nco, kt = tile / nco;
+  const int co0 = cot * TCo;
+  const int k0 = kt * TK;
+  int tap = 0, ci0 = 0;
+  if (!FIRST) { tap = k0 / a.Cin; ci0 = k0 - tap * a.Cin; }
+  const int kh = (a.ksize == 3) ? tap / 3 : 1, kw = (a.ksize == 3) ? tap % 3 : 1;
+  const int dh = (kh - 1) * a.dil, dw = (kw - 1) * a.dil;
+  const bool do_bias = (a.wsb != nullptr) && (kt == 0);
+
+  const int mbeg = slice * a.mslice;
+  const int mend = min(a.M, mbeg + a.mslice);
+  const int nstage = (mend > mbeg) ? (mend - mbeg + BKM - 1) / BKM : 0;
+  const int HW = a.H * a.W;
+
+  // per-thread rows (fixed offsets within a stage)
+  int arow[NA], ac[NA], brow[NB], bc[NB];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) { const int id = tid + 256 * i; arow[i] = id / CA; ac[i] = id % CA; }
+#pragma unroll
+  for (int i = 0; i < NB; ++i) { const int id = tid + 256 * i; brow[i] = id / CB; bc[i] = id % CB; }
+  // incremental (oh, ow) of each B row
+  int boh[NB], bow[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int m = mbeg + brow[i];
+    const int r = m % HW;
+    boh[i] = r / a.W; bow[i] = r % a.W;
+  }
+
+  uint4 ra[NA], rb[NB];
+  auto load_stage = [&](int st) {
+    const int m0 = mbeg + st * BKM;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int m = m0 + arow[i];
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (m < mend) v = *reinterpret_cast<const uint4*>(a.dy + (size_t)m * a.Cout + co0 + ac[i] * 8);
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int m = m0 + brow[i];
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (!FIRST) {
+        const int ih = boh[i] + dh, iw = bow[i] + dw;
+        if (m < mend && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+          v = *reinterpret_cast<const uint4*>(a.x + (size_t)(m + dh * a.W + dw) * a.Cin + ci0 + bc[i] * 8);
+      } else {
+        uint2 h2[2] = {make_uint2(0, 0), make_uint2(0, 0)};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int t = bc[i] * 2 + h;
+          if (t < 9 && m < mend) {
+            const int ddh = (t / 3 - 1) * a.dil, ddw = (t % 3 - 1) * a.dil;
+            const int ih = boh[i] + ddh, iw = bow[i] + ddw;
+            if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+              h2[h] = *reinterpret_cast<const uint2*>(a.x + (size_t)(m + ddh * a.W + ddw) * 4);
+          }
+        }
+        v = make_uint4(h2[0].x, h2[0].y, h2[1].x, h2[1].y);
+      }
+      rb[i] = v;
+      // advance this row by BKM pixels for the next stage
+      int ow = bow[i] + BKM, oh = boh[i];
+      while (ow >= a.W) { ow -= a.W; ++oh; }
+      while (oh >= a.H) oh -= a.H;
+      bow[i] = ow; boh[i] = oh;
+    }
+  };
+  auto store_stage = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      bf16_t* row = As + (buf * BKM + arow[i]) * TCo;
+      *reinterpret_cast<uint4*>(row + swz8<TCo>(arow[i], ac[i] * 2) * 4) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      bf16_t* row = Bs + (buf * BKM + brow[i]) * TK;
+      *reinterpret_cast<uint4*>(row + swz8<TK>(brow[i], bc[i] * 2) * 4) = rb[i];
+    }
+  };
+
+  f32x4 acc[4][4];
+  f32x4 accb[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    accb[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  bf16x8_t ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+
+  // transposed fragment read: 8 consecutive pixels (rows) of one column
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  auto read_frag = [&](const bf16_t* base, int rw_is128, int prow0, int col0) -> bf16x8_t {
+    s16x4 lo, hi;
+    const int r0 = prow0 + 8 * g + q;
+    const int c8 = (col0 >> 2) + p;
+    if (rw_is128) {
+      lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + r0 * 128 + swz8<128>(r0, c8) * 4));
+      hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + (r0 + 4) * 128 + swz8<128>(r0 + 4, c8) * 4));
+    } else {
+      lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + r0 * 64 + swz8<64>(r0, c8) * 4));
+      hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + (r0 + 4) * 64 + swz8<64>(r0 + 4, c8) * 4));
+    }
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8_t, v);
+  };
+
+  if (nstage > 0) {
+    load_stage(0);
+    store_stage(0);
+  }
+  __syncthreads();
+  for (int st = 0; st < nstage; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < nstage) load_stage(st + 1);
+    const bf16_t* Ab = As + buf * BKM * TCo;
+    const bf16_t* Bb = Bs + buf * BKM * TK;
+#pragma unroll
+    for (int kk = 0; kk < KSUB; ++kk) {
+      const int prow0 = wm * (32 * KSUB) + kk * 32;
+      bf16x8_t af[4], bfr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) af[j] = read_frag(Ab, TCo == 128, prow0, wc * 64 + j * 16);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bfr[i] = read_frag(Bb, TK == 128, prow0, wk * 64 + i * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], bfr[i], acc[j][i], 0, 0, 0);
+      if (do_bias) {
+        if (WM == 1) {
+          // wave (wc, wk) sums co tiles {2wk, 2wk+1}
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) {
+            const int j = 2 * wk + jj;
+            accb[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], ones, accb[j], 0, 0, 0);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            accb[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], ones, accb[j], 0, 0, 0);
+        }
+      }
+    }
+    if (st + 1 < nstage) store_stage(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue.  D layout: col = lane&15 -> k, rows (lane>>4)*4 + r -> co
+  const int fr = lane & 15, fq = lane >> 4;
+  float* slab = a.ws + (size_t)slice * a.Ktot * a.Cout;
+  if (WM == 1) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = k0 + wk * 64 + i * 16 + fr;
+        const int co = co0 + wc * 64 + j * 16 + fq * 4;
+        *reinterpret_cast<f32x4*>(slab + (size_t)k * a.Cout + co) = acc[j][i];
+      }
+    if (do_bias && fr == 0) {
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int j = 2 * wk + jj;
+        const int co = co0 + wc * 64 + j * 16 + fq * 4;
+        *reinterpret_cast<f32x4*>(a.wsb + (size_t)slice * a.Cout + co) = accb[j];
+      }
+    }
+  } else {
+    // sum the 4 pixel-quarter partials through LDS (staging buffers are free now)
+    float* red = reinterpret_cast<float*>(smem);   // [4 waves][16 tiles][64 lanes][4]
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        *reinterpret_cast<f32x4*>(red + ((wave * 16 + j * 4 + i) * 64 + lane) * 4) = acc[j][i];
+    float* redb = red + 4 * 16 * 64 * 4;          // [4 waves][4][64][4]
+    if (do_bias) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) *reinterpret_cast<f32x4*>(redb + ((wave * 4 + j) * 64 + lane) * 4) = accb[j];
+    }
+    __syncthreads();
+    // wave w reduces tiles j = w (4 i-tiles each)
+    const int j = wave;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int w = 0; w < 4; ++w) s += *reinterpret_cast<const f32x4*>(red + ((w * 16 + j * 4 + i) * 64 + lane) * 4);
+      const int k = k0 + i * 16 + fr;
+      const int co = co0 + j * 16 + fq * 4;
+      *reinterpret_cast<f32x4*>(slab + (size_t)k * a.Cout + co) = s;
+    }
+    if (do_bias && fr == 0) {
+      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int w = 0; w < 4; ++w) s += *reinterpret_cast<const f32x4*>(redb + ((w * 4 + j) * 64 + lane) * 4);
+      const int co = co0 + j * 16 + fq * 4;
+      *reinterpret_cast<f32x4*>(a.wsb + (size_t)slice * a.Cout + co) = s;
+    }
+  }
+}
+
+// Sum S slabs [S][Ktot][Cout] in fixed order and write dW in the PyTorch
+// layout [Cout][Cin][kh][kw] (first layer: Cin = 3 real channels of the
+// k = tap*4 + c packing).  beta = 0 overwrites, 1 accumulates.
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ ws, const float* __restrict__ wsb,
+                                                           float* __restrict__ dw, float* __restrict__ db, int S,
+                                                           int Ktot, int Cout, int Cin, int taps, int first,
+                                                           float beta, float scale) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;   // over Ktot*Cout, co fastest
+  const size_t plane = (size_t)Ktot * Cout;
+  if (idx < plane) {
+    float s = 0.f;
+    for (int sl = 0; sl < S; ++sl) s += ws[sl * plane + idx];
+    s *= scale;
+    const int co = idx % Cout, k = idx / Cout;
+    int ci, tap;
+    bool valid = true;
+    if (first) { tap = k >> 2; ci = k & 3; valid = (tap < 9) && (ci < 3); }
+    else { tap = k / Cin; ci = k - tap * Cin; }
+    if (valid) {
+      const int cin_t = first ? 3 : Cin;
+      float* o = dw + ((size_t)co * cin_t + ci) * taps + tap;
+      *o = (beta != 0.f) ? (*o * beta + s) : s;
+    }
+  }
+  if (db != nullptr && idx < Cout) {
+    float s = 0.f;
+    for (int sl = 0; sl < S; ++sl) s += wsb[(size_t)sl * Cout + idx];
+    s *= scale;
+    db[idx] = (beta != 0.f) ? (db[idx] * beta + s) : s;
+  }
+}
+
+template <int WC, int WK, int WM, bool FIRST>
+static int launch_wgrad(const WgradArgs& a, hipStream_t s) {
+  constexpr int TCo = 64 * WC, TK = 64 * WK;
+  constexpr int KSUB = (WM == 1) ? 2 : 1;
+  constexpr int BKM = 32 * KSUB * WM;
+  size_t lds = 2 * BKM * (TCo + TK) * 2;
+  if (WM != 1) lds = std::max(lds, (size_t)(4 * 16 * 64 * 4 + 4 * 4 * 64 * 4) * 4);
+  auto kfn = conv_wgrad_kernel<WC, WK, WM, FIRST>;
+  static bool attr = false;
+  if (!attr) {
+    CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  const int ntile = (a.Cout / TCo) * (a.Ktot / TK);
+  hipLaunchKernelGGL(kfn, dim3(ntile * a.S), dim3(256), lds, s, a);
+  return (int)hipGetLastError();
+}
+
+}  // namespace can
+
+// Workspace needed (floats) for a given split; the Python side sizes one
+// shared workspace for the largest layer.
+extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, int target_blocks, int* S_out,
+                              int* mslice_out, int* cfg_out) {
+  const int Ktot = first ? 64 : ksize * ksize * Cin;
+  const int cfg = (!first && Cout % 128 == 0 && Cin % 128 == 0) ? 1 : 2;
+  const int TCo = cfg == 1 ? 128 : 64, TK = cfg == 1 ? 128 : 64;
+  const int BKM = cfg == 1 ? 64 : 128;
+  const int ntile = (Cout / TCo) * (Ktot / TK);
+  int S = (target_blocks + ntile - 1) / ntile;
+  const int max_s = (M + BKM - 1) / BKM;
+  if (S > max_s) S = max_s;
+  if (S < 1) S = 1;
+  int mslice = (M + S - 1) / S;
+  mslice = ((mslice + BKM - 1) / BKM) * BKM;
+  S = (M + mslice - 1) / mslice;
+  *S_out = S; *mslice_out = mslice; *cfg_out = cfg;
+  return 0;
+}
+
+extern "C" int can_conv_wgrad(const void* dy, const void* x, float* ws, float* wsb, float* dw, float* db, int N,
+                              int H, int W, int Cin, int Cout, int ksize, int dil, int first, int S, int mslice,
+                              int cfg, float beta, float scale, void* stream) {
+  using namespace can;
+  WgradArgs a;
+  a.dy = (const bf16_t*)dy; a.x = (const bf16_t*)x; a.ws = ws; a.wsb = (db != nullptr) ? wsb : nullptr;
+  a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.ksize = ksize; a.dil = dil; a.M = N * H * W;
+  a.Ktot = first ? 64 : ksize * ksize * Cin; a.S = S; a.mslice = mslice;
+  hipStream_t s = (hipStream_t)stream;
+  int rc;
+  if (first) {
+    if (Cin != 4 || Cout % 64) return -2;
+    rc = launch_wgrad<1, 1, 4, true>(a, s);
+  } else if (cfg == 1) {
+    if (Cout % 128 || Cin % 128) return -3;
+    rc = launch_wgrad<2, 2, 1, false>(a, s);
+  } else {
+    if (Cout % 64 || Cin % 64) return -4;
+    rc = launch_wgrad<1, 1, 4, false>(a, s);
+  }
+  if (rc) return rc;
+  const int plane = a.Ktot * Cout;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((plane + 255) / 256), dim3(256), 0, s, ws, a.wsb, dw, db, S, a.Ktot,
+                     Cout, first ? 4 : Cin, ksize * ksize, first, beta, scale);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,300 @@
+// Memory-bound kernels of the CANNet step (gfx950): all NHWC bf16, 16-B
+// vectorised per lane (8 channels), grid-stride, no atomics on hot paths.
+//
+//   maxpool2x2_fwd      nn.MaxPool2d(2,2)                  model/CANNet.py:112
+//   maxpool2x2_bwd_relu max_pool2d_with_indices_backward + threshold_backward
+//                       (gather form: first-max-in-window wins, as ATen; the
+//                       ReLU mask of the pooled layer is folded in)
+//   head_fwd            output_layer 1x1 64->1 + bias       model/CANNet.py:17,90
+//   head_train          head fwd + MSELoss(sum) + its backward + ReLU mask of
+//                       the last backend layer, one pass      utils/train_eval_utils.py:20,37-38
+//   sgd_momentum        torch.optim.SGD(momentum=0.95) step over the flat fp32
+//                       arena, gradient averaging folded in, skipped on a
+//                       device-side non-finite flag             train.py:126
+//   pack_conv           fp32 [Co][Ci][kh][kw] -> bf16 forward / dgrad packs
+//   img_to_nhwc4        [N,3,H,W] fp32 -> [N,H,W,4] bf16 (first-layer input)
+#include "common.h"
+
+namespace can {
+
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+  const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  return make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
+}
+// bf16 compare helpers on raw bits (order-preserving map)
+__device__ __forceinline__ float bfv(unsigned short b) { return __uint_as_float(((unsigned)b) << 16); }
+
+// ---------------------------------------------------------------- maxpool
+__global__ void __launch_bounds__(256) maxpool_fwd_kernel(const uint4* __restrict__ x, uint4* __restrict__ y, int N,
+                                                          int H, int W, int C8) {
+  const int Ho = H >> 1, Wo = W >> 1;
+  const size_t total = (size_t)N * Ho * Wo * C8;
+  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const int c = i % C8;
+    size_t p = i / C8;
+    const int ox = p % Wo; p /= Wo;
+    const int oy = p % Ho; const int n = p / Ho;
+    const size_t base = (((size_t)n * H + 2 * oy) * W + 2 * ox) * C8 + c;
+    float a[8], b[8], m[8];
+    unpack8(x[base], m);
+    unpack8(x[base + C8], a);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m[k] = fmaxf(m[k], a[k]);
+    unpack8(x[base + (size_t)W * C8], a);
+    unpack8(x[base + (size_t)W * C8 + C8], b);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m[k] = fmaxf(m[k], fmaxf(a[k], b[k]));
+    y[i] = pack8(m);  // exact: max of bf16 values is a bf16 value
+  }
+}
+
+// dx[full] = (x is the first max of its window) * (x > 0) * dy[pooled]
+__global__ void __launch_bounds__(256) maxpool_bwd_relu_kernel(const uint4* __restrict__ x, const uint4* __restrict__ dy,
+                                                               uint4* __restrict__ dx, int N, int H, int W, int C8) {
+  const int Ho = H >> 1, Wo = W >> 1;
+  const size_t total = (size_t)N * Ho * Wo * C8;
+  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const int c = i % C8;
+    size_t p = i / C8;
+    const int ox = p % Wo; p /= Wo;
+    const int oy = p % Ho; const int n = p / Ho;
+    const size_t b0 = (((size_t)n * H + 2 * oy) * W + 2 * ox) * C8 + c;
+    const size_t off[4] = {b0, b0 + C8, b0 + (size_t)W * C8, b0 + (size_t)W * C8 + C8};
+    float v[4][8], g[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) unpack8(x[off[q]], v[q]);
+    unpack8(dy[i], g);
+    float o[4][8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      // ATen scan order: (0,0),(0,1),(1,0),(1,1); strict '>' keeps the first max
+      int arg = 0;
+      float mv = v[0][k];
+#pragma unroll
+      for (int q = 1; q < 4; ++q)
+        if (v[q][k] > mv) { mv = v[q][k]; arg = q; }
+      const float gg = (mv > 0.f) ? g[k] : 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q][k] = (q == arg) ? gg : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dx[off[q]] = pack8(o[q]);
+  }
+}
+
+// ---------------------------------------------------------------- head
+// et[p] = sum_c y[p][c] * w[c] + b      (y: [P][64] bf16 post-ReLU)
+__global__ void __launch_bounds__(256) head_fwd_kernel(const uint4* __restrict__ y, const float* __restrict__ w,
+                                                       const float* __restrict__ b, float* __restrict__ et, int P) {
+  // 8 lanes per pixel (8 channels each)
+  const int lane8 = threadIdx.x & 7;
+  float wl[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) wl[k] = w[lane8 * 8 + k];
+  const float bias = b[0];
+  for (size_t p = ((size_t)blockIdx.x * 256 + threadIdx.x) >> 3; p < (size_t)P; p += ((size_t)gridDim.x * 256) >> 3) {
+    float v[8];
+    unpack8(y[p * 8 + lane8], v);
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += v[k] * wl[k];
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 4, 64);
+    if (lane8 == 0) et[p] = s + bias;
+  }
+}
+
+// Training head: et = y.w + b; loss = sum (et-gt)^2; det = 2(et-gt)*gscale;
+// dy[p][c] = det * w[c] * (y > 0); partial dw[c] = sum_p det*y[p][c], db = sum det.
+// Per-block partials -> part[block][66] (64 dw, db, loss); reduced by head_reduce.
+__global__ void __launch_bounds__(256) head_train_kernel(const uint4* __restrict__ y, const float* __restrict__ w,
+                                                         const float* __restrict__ b, const float* __restrict__ gt,
+                                                         float* __restrict__ et, uint4* __restrict__ dy,
+                                                         float* __restrict__ part, int P, float gscale) {
+  __shared__ float red[256 / 8][66];
+  const int lane8 = threadIdx.x & 7;
+  const int pg = threadIdx.x >> 3;
+  float wl[8], dwl[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { wl[k] = w[lane8 * 8 + k]; dwl[k] = 0.f; }
+  const float bias = b[0];
+  float dbl = 0.f, lossl = 0.f;
+  for (size_t p = ((size_t)blockIdx.x * 256 + threadIdx.x) >> 3; p < (size_t)P; p += ((size_t)gridDim.x * 256) >> 3) {
+    float v[8];
+    unpack8(y[p * 8 + lane8], v);
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += v[k] * wl[k];
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 4, 64);
+    const float e = s + bias;
+    const float d = e - gt[p];
+    const float g = 2.f * d * gscale;
+    if (lane8 == 0) { et[p] = e; lossl += d * d; dbl += g; }
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      o[k] = (v[k] > 0.f) ? g * wl[k] : 0.f;
+      dwl[k] += g * v[k];
+    }
+    dy[p * 8 + lane8] = pack8(o);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[pg][lane8 * 8 + k] = dwl[k];
+  if (lane8 == 0) { red[pg][64] = dbl; red[pg][65] = lossl; }
+  __syncthreads();
+  if (threadIdx.x < 66) {
+    float s = 0.f;
+    for (int r = 0; r < 256 / 8; ++r) s += red[r][threadIdx.x];
+    part[(size_t)blockIdx.x * 66 + threadIdx.x] = s;
+  }
+}
+
+// out[0..63] = dw, out[64] = db, loss_out[0] = loss  (fixed-order, deterministic)
+__global__ void __launch_bounds__(128) head_reduce_kernel(const float* __restrict__ part, int nblk,
+                                                          float* __restrict__ dw, float* __restrict__ db,
+                                                          float* __restrict__ loss, float beta) {
+  const int t = threadIdx.x;
+  if (t < 66) {
+    float s = 0.f;
+    for (int i = 0; i < nblk; ++i) s += part[(size_t)i * 66 + t];
+    if (t < 64) dw[t] = (beta != 0.f) ? dw[t] * beta + s : s;
+    else if (t == 64) db[0] = (beta != 0.f) ? db[0] * beta + s : s;
+    else loss[0] = s;
+  }
+}
+
+// ---------------------------------------------------------------- SGD
+// torch.optim.SGD semantics (dampening 0, nesterov False, wd 0):
+//   buf = g (first step) | momentum*buf + g ;  p -= lr*buf,  g = grad*gscale.
+// flags[0] != 0 (non-finite loss) -> the whole update is skipped (graph-safe,
+// no host sync).  Vectorised float4 over a 16-B aligned arena.
+__global__ void __launch_bounds__(256) sgd_momentum_kernel(float4* __restrict__ p, float4* __restrict__ buf,
+                                                           const float4* __restrict__ g, size_t n4, float lr,
+                                                           float momentum, float gscale, int first,
+                                                           const float* __restrict__ flags) {
+  if (flags != nullptr && flags[0] != 0.f) return;
+  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+    float4 gv = g[i];
+    gv.x *= gscale; gv.y *= gscale; gv.z *= gscale; gv.w *= gscale;
+    float4 b;
+    if (first) b = gv;
+    else {
+      b = buf[i];
+      b.x = momentum * b.x + gv.x; b.y = momentum * b.y + gv.y;
+      b.z = momentum * b.z + gv.z; b.w = momentum * b.w + gv.w;
+    }
+    buf[i] = b;
+    float4 pv = p[i];
+    pv.x -= lr * b.x; pv.y -= lr * b.y; pv.z -= lr * b.z; pv.w -= lr * b.w;
+    p[i] = pv;
+  }
+}
+
+// ---------------------------------------------------------------- packing
+// w fp32 [Co][Ci][k][k] -> fwd bf16 [Co][tap][Ci] and dgrad bf16 [Ci][8-tap][Co]
+// (first layer: fwd [Co][64] with k = tap*4 + c, no dgrad).
+__global__ void __launch_bounds__(256) pack_conv_kernel(const float* __restrict__ w, bf16_t* __restrict__ fwd,
+                                                        bf16_t* __restrict__ dgr, int Co, int Ci, int taps,
+                                                        int first) {
+  const size_t total = (size_t)Co * Ci * taps;
+  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const int tap = i % taps;
+    const size_t r = i / taps;
+    const int ci = r % Ci;
+    const int co = r / Ci;
+    const unsigned short v = f2bf(w[i]);
+    if (first) {
+      fwd[(size_t)co * 64 + tap * 4 + ci] = v;
+    } else {
+      fwd[((size_t)co * taps + tap) * Ci + ci] = v;
+      if (dgr) dgr[((size_t)ci * taps + (taps - 1 - tap)) * Co + co] = v;
+    }
+  }
+}
+
+// [N,3,H,W] fp32 -> [N,H,W,4] bf16 (4th channel zero)
+__global__ void __launch_bounds__(256) img_to_nhwc4_kernel(const float* __restrict__ img, uint2* __restrict__ out,
+                                                           int N, int H, int W) {
+  const size_t HW = (size_t)H * W;
+  const size_t total = (size_t)N * HW;
+  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const size_t n = i / HW, p = i % HW;
+    const float* b = img + n * 3 * HW + p;
+    out[i] = make_uint2(pack2bf(b[0], b[HW]), pack2bf(b[2 * HW], 0.f));
+  }
+}
+
+static inline int grid_for(size_t n, int per = 256, int cap = 4096) {
+  size_t g = (n + per - 1) / per;
+  if (g > (size_t)cap) g = cap;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace can
+
+using namespace can;
+
+extern "C" int can_maxpool_fwd(const void* x, void* y, int N, int H, int W, int C, void* stream) {
+  if ((C & 7) || (H & 1) || (W & 1)) return -2;
+  const size_t tot = (size_t)N * (H / 2) * (W / 2) * (C / 8);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(tot, 256, 8192)), dim3(256), 0, (hipStream_t)stream,
+                     (const uint4*)x, (uint4*)y, N, H, W, C / 8);
+  return (int)hipGetLastError();
+}
+
+extern "C" int can_maxpool_bwd_relu(const void* x, const void* dy, void* dx, int N, int H, int W, int C,
+                                    void* stream) {
+  if ((C & 7) || (H & 1) || (W & 1)) return -2;
+  const size_t tot = (size_t)N * (H / 2) * (W / 2) * (C / 8);
+  hipLaunchKernelGGL(maxpool_bwd_relu_kernel, dim3(grid_for(tot, 256, 8192)), dim3(256), 0, (hipStream_t)stream,
+                     (const uint4*)x, (const uint4*)dy, (uint4*)dx, N, H, W, C / 8);
+  return (int)hipGetLastError();
+}
+
+extern "C" int can_head_fwd(const void* y, const float* w, const float* b, float* et, int P, void* stream) {
+  hipLaunchKernelGGL(head_fwd_kernel, dim3(grid_for((size_t)P * 8, 256, 2048)), dim3(256), 0, (hipStream_t)stream,
+                     (const uint4*)y, w, b, et, P);
+  return (int)hipGetLastError();
+}
+
+extern "C" int can_head_train(const void* y, const float* w, const float* b, const float* gt, float* et, void* dy,
+                              float* part, int nblk, float* dw, float* db, float* loss, int P, float gscale,
+                              float beta, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(head_train_kernel, dim3(nblk), dim3(256), 0, s, (const uint4*)y, w, b, gt, et, (uint4*)dy, part,
+                     P, gscale);
+  hipLaunchKernelGGL(head_reduce_kernel, dim3(1), dim3(128), 0, s, part, nblk, dw, db, loss, beta);
+  return (int)hipGetLastError();
+}
+
+extern "C" int can_sgd_momentum(float* p, float* buf, const float* g, size_t n, float lr, float momentum,
+                                float gscale, int first, const float* flags, void* stream) {
+  if (n & 3) return -2;
+  hipLaunchKernelGGL(sgd_momentum_kernel, dim3(grid_for(n / 4, 256, 4096)), dim3(256), 0, (hipStream_t)stream,
+                     (float4*)p, (float4*)buf, (const float4*)g, n / 4, lr, momentum, gscale, first, flags);
+  return (int)hipGetLastError();
+}
+
+extern "C" int can_pack_conv(const float* w, void* fwd, void* dgr, int Co, int Ci, int taps, int first,
+                             void* stream) {
+  hipLaunchKernelGGL(pack_conv_kernel, dim3(grid_for((size_t)Co * Ci * taps, 256, 4096)), dim3(256), 0,
+                     (hipStream_t)stream, w, (bf16_t*)fwd, (bf16_t*)dgr, Co, Ci, taps, first);
+  return (int)hipGetLastError();
+}
+
+extern "C" int can_img_to_nhwc4(const float* img, void* out, int N, int H, int W, void* stream) {
+  hipLaunchKernelGGL(img_to_nhwc4_kernel, dim3(grid_for((size_t)N * H * W, 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, img, (uint2*)out, N, H, W);
+  return (int)hipGetLastError();
+}

@@ -103,3 +103,58 @@ def conv_igemm(x: torch.Tensor, wpack: torch.Tensor, bias: Optional[torch.Tensor
                  mask.data_ptr() if mask is not None else 0, out.data_ptr(), n, h, w, ci, co, ksize, dil,
                  epi, int(first), tile, _ext.stream_ptr(x.device))
     return out
+
+
+class WgradWorkspace:
+    """One fp32 scratch buffer for the split-pixel partial slabs, grown on demand
+    (allocated outside any captured region, never inside a launch function)."""
+
+    def __init__(self, device, target_blocks: int = 1024):
+        self.device = torch.device(device)
+        self.target_blocks = target_blocks
+        self.buf = torch.empty(0, dtype=torch.float32, device=self.device)
+
+    def plan(self, m: int, ci: int, co: int, ksize: int, first: bool):
+        C = _ext.require()
+        s, mslice, cfg = C.wgrad_plan(m, ci, co, ksize, int(first), self.target_blocks)
+        ktot = 64 if first else ksize * ksize * ci
+        need = s * ktot * co + s * co
+        return s, mslice, cfg, need
+
+    def reserve(self, need: int) -> torch.Tensor:
+        if self.buf.numel() < need:
+            self.buf = torch.empty(need, dtype=torch.float32, device=self.device)
+        return self.buf
+
+
+def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, db: Optional[torch.Tensor], *, ksize: int,
+               dil: int = 1, first: bool = False, ws: Optional[WgradWorkspace] = None, beta: float = 0.0,
+               scale: float = 1.0) -> None:
+    """dw[Co,Ci,kh,kw] (fp32, PyTorch layout) = scale * sum_m dY[m,co] Xcol[m,k] (+ beta*dw); db likewise."""
+    C = _ext.require()
+    _check_act(dy, "dy")
+    _check_act(x, "x")
+    n, h, w, ci = x.shape
+    co = dy.shape[-1]
+    if tuple(dy.shape[:3]) != (n, h, w):
+        raise ValueError("dy/x spatial mismatch")
+    if first:
+        if ci != 4 or ksize != 3 or tuple(dw.shape) != (co, 3, 3, 3):
+            raise ValueError("first-layer wgrad expects x[...,4] and dw[Co,3,3,3]")
+    else:
+        if ci % 64 or co % 64:
+            raise ValueError("Cin/Cout must be multiples of 64")
+        if tuple(dw.shape) != (co, ci, ksize, ksize):
+            raise ValueError(f"dw shape {tuple(dw.shape)} != {(co, ci, ksize, ksize)}")
+    if dw.dtype != torch.float32 or not dw.is_contiguous():
+        raise ValueError("dw must be contiguous fp32")
+    if db is not None and (db.dtype != torch.float32 or db.numel() != co or not db.is_contiguous()):
+        raise ValueError("db must be contiguous fp32 [Co]")
+    ws = ws or WgradWorkspace(x.device)
+    s, mslice, cfg, need = ws.plan(n * h * w, ci, co, ksize, first)
+    buf = ws.reserve(need)
+    ktot = 64 if first else ksize * ksize * ci
+    wsb_ptr = buf.data_ptr() + 4 * s * ktot * co
+    C.conv_wgrad(dy.data_ptr(), x.data_ptr(), buf.data_ptr(), wsb_ptr, dw.data_ptr(),
+                 db.data_ptr() if db is not None else 0, n, h, w, ci, co, ksize, dil, int(first), s, mslice, cfg,
+                 float(beta), float(scale), _ext.stream_ptr(x.device))

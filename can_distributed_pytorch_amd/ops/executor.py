@@ -1,0 +1,377 @@
+"""Native CANNet executor: a static, hand-scheduled forward/backward over the
+gfx950 kernels (no tracing compiler, no autograd graph of ATen ops).
+
+Reference math: model/CANNet.py:39-91 (forward), the backward is what
+autograd derives for it in the reference (SURVEY §2.5 kernel inventory).
+
+Data layout: NHWC bf16 activations, fp32 master weights in the model's own
+nn.Parameters, bf16 packed weight copies (forward + flipped dgrad layouts)
+refreshed by one pack kernel per layer whenever the fp32 weights change.
+
+Forward (training) saves exactly what the backward needs: every conv input
+(NHWC bf16), the pre-pool activations, the context tables, c_S and w_S.
+Backward (per layer, reverse order) = weight-gradient (split-pixel MFMA +
+deterministic slab reduction) + data-gradient (same MFMA kernel as forward,
+flipped weights, ReLU mask / maxpool-backward fused), and after each layer's
+gradients are written a ``on_grad_ready(param_indices)`` callback fires so
+a bucketed reducer can start all-reducing while the remaining layers run.
+
+Two ways in:
+  * ``executor(x)``            — autograd-compatible (CANNet.forward on GPU):
+                                 an autograd.Function whose backward returns
+                                 ordinary gradients.
+  * ``forward_train / backward_from_head`` — used by the native training step
+                                 (engine/native.py): gradients go straight into
+                                 caller-provided fp32 buffers (the flat gradient
+                                 arena), the head/MSE loss is fused.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, Dict, List, Optional, Sequence
+
+import torch
+import torch.nn as nn
+
+from . import _ext
+from . import conv as C
+from ..models.cannet import CONTEXT_SCALES
+
+BF16 = torch.bfloat16
+CELL_OFF = {1: 0, 2: 1, 3: 5, 6: 14}
+
+
+@dataclass
+class ConvSpec:
+    idx: int                 # position in the executor's conv list
+    module: nn.Conv2d
+    cin: int
+    cout: int
+    ksize: int
+    dil: int
+    first: bool = False
+    pool_after: bool = False  # a 2x2 maxpool follows this conv's ReLU
+    w_index: int = -1         # index of weight in model.parameters()
+    b_index: int = -1
+
+
+class CANNetExecutor:
+    def __init__(self, model: nn.Module):
+        self.C = _ext.require()
+        self.model = model
+        params = list(model.parameters())
+        pid = {id(p): i for i, p in enumerate(params)}
+        self.n_params = len(params)
+        self.front: List[ConvSpec] = []
+        mods = list(model.frontend)
+        convs = [m for m in mods if isinstance(m, nn.Conv2d)]
+        for j, m in enumerate(convs):
+            k = mods.index(m)
+            pool_after = any(isinstance(mods[t], nn.MaxPool2d) for t in range(k + 1, min(k + 3, len(mods))))
+            self.front.append(ConvSpec(j, m, m.in_channels, m.out_channels, 3, 1, first=(j == 0),
+                                       pool_after=pool_after, w_index=pid[id(m.weight)], b_index=pid[id(m.bias)]))
+        self.back: List[ConvSpec] = []
+        for j, m in enumerate([m for m in model._modules["backend"] if isinstance(m, nn.Conv2d)]):
+            self.back.append(ConvSpec(j, m, m.in_channels, m.out_channels, 3, m.dilation[0],
+                                      w_index=pid[id(m.weight)], b_index=pid[id(m.bias)]))
+        self.head = model.output_layer
+        self.head_w_index, self.head_b_index = pid[id(self.head.weight)], pid[id(self.head.bias)]
+        self.ctx1 = {s: getattr(model, f"conv{s}_1") for s in CONTEXT_SCALES}
+        self.ctx2 = {s: getattr(model, f"conv{s}_2") for s in CONTEXT_SCALES}
+        self.ctx1_index = {s: pid[id(self.ctx1[s].weight)] for s in CONTEXT_SCALES}
+        self.ctx2_index = {s: pid[id(self.ctx2[s].weight)] for s in CONTEXT_SCALES}
+        self.packs: Dict[int, tuple] = {}
+        self._pack_version = None
+        self.ws = None
+        self.stream_override = None
+
+    # ----------------------------------------------------------- weights
+    def _params(self):
+        return list(self.model.parameters())
+
+    def _weights_version(self):
+        return tuple(p._version for p in self._params())
+
+    def _alloc_packs(self, device):
+        for s in self.front + self.back:
+            w = s.module.weight
+            if s.first:
+                fwd = torch.empty(s.cout, 64, dtype=BF16, device=device)
+                dgr = None
+            else:
+                fwd = torch.empty(s.cout, s.ksize * s.ksize * s.cin, dtype=BF16, device=device)
+                dgr = torch.empty(s.cin, s.ksize * s.ksize * s.cout, dtype=BF16, device=device)
+            self.packs[id(w)] = (fwd, dgr)
+        for sc in CONTEXT_SCALES:
+            w = self.ctx2[sc].weight
+            self.packs[id(w)] = (torch.empty(512, 512, dtype=BF16, device=device),
+                                 torch.empty(512, 512, dtype=BF16, device=device))
+
+    def refresh_packs(self, force: bool = False):
+        """Re-pack bf16 weight copies from the fp32 masters (one kernel per layer)."""
+        ver = self._weights_version()
+        if not force and ver == self._pack_version and self.packs:
+            return
+        dev = self.head.weight.device
+        if not self.packs:
+            self._alloc_packs(dev)
+        st = self._stream()
+        for s in self.front + self.back:
+            w = s.module.weight.detach()
+            fwd, dgr = self.packs[id(s.module.weight)]
+            self.C.pack_conv(w.data_ptr(), fwd.data_ptr(), dgr.data_ptr() if dgr is not None else 0, s.cout, s.cin,
+                             s.ksize * s.ksize, int(s.first), st)
+        for sc in CONTEXT_SCALES:
+            w = self.ctx2[sc].weight.detach()
+            fwd, dgr = self.packs[id(self.ctx2[sc].weight)]
+            self.C.pack_conv(w.data_ptr(), fwd.data_ptr(), dgr.data_ptr(), 512, 512, 1, 0, st)
+        self._pack_version = ver
+
+    def mark_weights_updated(self):
+        """Called by the fused optimizer after it has re-packed (keeps versions in sync)."""
+        self._pack_version = self._weights_version()
+
+    def _stream(self):
+        return self.stream_override if self.stream_override is not None else _ext.stream_ptr()
+
+    def workspace(self, n, h, w):
+        """Size the shared wgrad slab workspace for an input of [n,3,h,w] (call before graph capture)."""
+        if self.ws is None:
+            self.ws = C.WgradWorkspace(self.head.weight.device)
+        need = 0
+        hh, ww = h, w
+        for s in self.front:
+            _, _, _, nd = self.ws.plan(n * hh * ww, 4 if s.first else s.cin, s.cout, 3, s.first)
+            need = max(need, nd)
+            if s.pool_after:
+                hh, ww = hh // 2, ww // 2
+        for s in self.back:
+            need = max(need, self.ws.plan(n * hh * ww, s.cin, s.cout, 3, False)[3])
+        need = max(need, self.ws.plan(n * hh * ww, 512, 512, 1, False)[3])
+        self.ws.reserve(need)
+        return self.ws
+
+    # ----------------------------------------------------------- forward
+    def _conv(self, s: ConvSpec, x, epi=C.EPI_BIAS_RELU):
+        fwd, _ = self.packs[id(s.module.weight)]
+        return C.conv_igemm(x, fwd, s.module.bias.detach(), ksize=s.ksize, dil=s.dil, epi=epi, first=s.first)
+
+    def _maxpool(self, x):
+        n, h, w, c = x.shape
+        y = torch.empty(n, h // 2, w // 2, c, dtype=BF16, device=x.device)
+        self.C.maxpool_fwd(x.data_ptr(), y.data_ptr(), n, h, w, c, self._stream())
+        return y
+
+    def _img(self, img):
+        if img.dim() != 4 or img.shape[1] != 3:
+            raise ValueError("input must be [N,3,H,W]")
+        n, _, h, w = img.shape
+        if h % 8 or w % 8:
+            raise ValueError(f"H, W must be multiples of 8 (got {h}x{w}); resize as CrowdDataset does")
+        img = img.float().contiguous()
+        x4 = torch.empty(n, h, w, 4, dtype=BF16, device=img.device)
+        self.C.img_to_nhwc4(img.data_ptr(), x4.data_ptr(), n, h, w, self._stream())
+        return x4
+
+    def forward_features(self, img, save: bool):
+        """Runs everything up to the last backend ReLU. Returns (b6 [N,h,w,64], saved dict)."""
+        self.refresh_packs()
+        sv = {} if save else None
+        x = self._img(img)
+        acts = []   # conv inputs of the frontend
+        pre_pool = {}
+        for s in self.front:
+            acts.append(x)
+            y = self._conv(s, x)
+            if s.pool_after:
+                pre_pool[s.idx] = y
+                x = self._maxpool(y)
+            else:
+                x = y
+        fv = x
+        cat, ctx_saved = self._context_fwd(fv, save)
+        x = cat
+        back_in = []
+        for s in self.back:
+            back_in.append(x)
+            x = self._conv(s, x)
+        if save:
+            sv.update(front_in=acts, pre_pool=pre_pool, fv=fv, ctx=ctx_saved, back_in=back_in, b6=x)
+        return x, sv
+
+    def _context_fwd(self, fv, save):
+        n, h, w, c = fv.shape
+        st = self._stream()
+        rowacc = torch.empty(n, h, 12, c, dtype=torch.float32, device=fv.device)
+        ave = torch.empty(n, 50, c, dtype=torch.float32, device=fv.device)
+        self.C.ctx_reduce(0, fv.data_ptr(), 0, 0, rowacc.data_ptr(), ave.data_ptr(), n, h, w, c, st)
+        table = torch.empty_like(ave)
+        for sc in CONTEXT_SCALES:
+            o, k = CELL_OFF[sc], sc * sc
+            w1 = self.ctx1[sc].weight.detach().view(c, c)
+            torch.matmul(ave[:, o:o + k], w1.t(), out=table[:, o:o + k])
+        cs = torch.empty(4, n, h, w, c, dtype=BF16, device=fv.device)
+        self.C.ctx_expand(fv.data_ptr(), table.data_ptr(), cs.data_ptr(), n, h, w, c, st)
+        wts = torch.empty(4, n, h, w, c, dtype=BF16, device=fv.device)
+        for i, sc in enumerate(CONTEXT_SCALES):
+            fwd, _ = self.packs[id(self.ctx2[sc].weight)]
+            C.conv_igemm(cs[i], fwd, None, ksize=1, epi=4, out=wts[i])   # EPI_SIGMOID
+        cat = torch.empty(n, h, w, 2 * c, dtype=BF16, device=fv.device)
+        self.C.ctx_fuse(fv.data_ptr(), wts.data_ptr(), table.data_ptr(), cat.data_ptr(), n, h, w, c, st)
+        saved = dict(ave=ave, table=table, cs=cs, wts=wts, rowacc=rowacc) if save else None
+        return cat, saved
+
+    def head_forward(self, b6):
+        n, h, w, _ = b6.shape
+        et = torch.empty(n, 1, h, w, dtype=torch.float32, device=b6.device)
+        self.C.head_fwd(b6.data_ptr(), self.head.weight.detach().data_ptr(), self.head.bias.detach().data_ptr(),
+                        et.data_ptr(), n * h * w, self._stream())
+        return et
+
+    @torch.no_grad()
+    def forward_eval(self, img):
+        b6, _ = self.forward_features(img, save=False)
+        return self.head_forward(b6)
+
+    # ----------------------------------------------------------- backward
+    def backward_features(self, sv, d_b6: torch.Tensor, grads: Sequence[Optional[torch.Tensor]],
+                          on_grad_ready: Optional[Callable[[List[int]], None]] = None, beta: float = 0.0,
+                          scale: float = 1.0):
+        """d_b6: grad wrt the PRE-activation of the last backend conv (ReLU already applied).
+
+        grads[i] is the fp32 output tensor for model.parameters()[i] (written, or
+        accumulated when beta=1).  Entries for the head must already be filled.
+        """
+        st = self._stream()
+        ws = self.ws or self.workspace(*self._shape_from(sv))
+        ready = on_grad_ready or (lambda idx: None)
+
+        def wg(spec_or_w, dy, x, ksize, dil, first, wi, bi):
+            C.conv_wgrad(dy, x, grads[wi], grads[bi] if bi is not None else None, ksize=ksize, dil=dil, first=first,
+                         ws=ws, beta=beta, scale=scale)
+            ready([wi] + ([bi] if bi is not None else []))
+
+        # ---- backend, reverse
+        dy = d_b6
+        for s in reversed(self.back):
+            x = sv["back_in"][s.idx]
+            wg(s, dy, x, 3, s.dil, False, s.w_index, s.b_index)
+            _, dgr = self.packs[id(s.module.weight)]
+            if s.idx > 0:
+                dy = C.conv_igemm(dy, dgr, None, ksize=3, dil=s.dil, epi=C.EPI_MASK, mask=x)
+            else:
+                dcat = C.conv_igemm(dy, dgr, None, ksize=3, dil=s.dil, epi=C.EPI_NONE)
+        # ---- context module
+        fv = sv["fv"]
+        ctx = sv["ctx"]
+        n, h, w, c = fv.shape
+        dz = torch.empty(4, n, h, w, c, dtype=BF16, device=fv.device)
+        sdir = torch.empty_like(dz)
+        self.C.ctx_bwd_e1(dcat.data_ptr(), ctx["wts"].data_ptr(), ctx["table"].data_ptr(), dz.data_ptr(),
+                          sdir.data_ptr(), n, h, w, c, st)
+        dc = torch.empty_like(dz)
+        for i, sc in enumerate(CONTEXT_SCALES):
+            _, dgr = self.packs[id(self.ctx2[sc].weight)]
+            C.conv_igemm(dz[i], dgr, None, ksize=1, epi=C.EPI_NONE, out=dc[i])
+            wi = self.ctx2_index[sc]
+            C.conv_wgrad(dz[i], ctx["cs"][i], grads[wi], None, ksize=1, ws=ws, beta=beta, scale=scale)
+        ready([self.ctx2_index[sc] for sc in CONTEXT_SCALES])
+        rowacc = ctx["rowacc"]
+        dA = torch.empty(n, 50, c, dtype=torch.float32, device=fv.device)
+        self.C.ctx_reduce(1, 0, sdir.data_ptr(), dc.data_ptr(), rowacc.data_ptr(), dA.data_ptr(), n, h, w, c, st)
+        dave = torch.empty_like(dA)
+        ave = ctx["ave"]
+        for sc in CONTEXT_SCALES:
+            o, k = CELL_OFF[sc], sc * sc
+            w1 = self.ctx1[sc].weight.detach().view(c, c)
+            gA = dA[:, o:o + k].reshape(-1, c)
+            g = grads[self.ctx1_index[sc]].view(c, c)
+            gw = gA.t() @ ave[:, o:o + k].reshape(-1, c)
+            if scale != 1.0:
+                gw = gw * scale
+            if beta:
+                g.add_(gw)
+            else:
+                g.copy_(gw)
+            torch.matmul(dA[:, o:o + k], w1, out=dave[:, o:o + k])
+        ready([self.ctx1_index[sc] for sc in CONTEXT_SCALES])
+        dfv = torch.empty(n, h, w, c, dtype=BF16, device=fv.device)
+        self.C.ctx_bwd_final(dcat.data_ptr(), dc.data_ptr(), dave.data_ptr(), fv.data_ptr(), dfv.data_ptr(), n, h, w,
+                             c, st)
+        # ---- frontend, reverse
+        dy = dfv
+        for s in reversed(self.front):
+            x = sv["front_in"][s.idx]
+            wg(s, dy, x, 3, 1, s.first, s.w_index, s.b_index)
+            if s.idx == 0:
+                break
+            _, dgr = self.packs[id(s.module.weight)]
+            prev = self.front[s.idx - 1]
+            if prev.pool_after:
+                dp = C.conv_igemm(dy, dgr, None, ksize=3, dil=1, epi=C.EPI_NONE)
+                full = sv["pre_pool"][prev.idx]
+                dfull = torch.empty_like(full)
+                nn_, hh, ww, cc = full.shape
+                self.C.maxpool_bwd_relu(full.data_ptr(), dp.data_ptr(), dfull.data_ptr(), nn_, hh, ww, cc, st)
+                dy = dfull
+            else:
+                dy = C.conv_igemm(dy, dgr, None, ksize=3, dil=1, epi=C.EPI_MASK, mask=x)
+
+    @staticmethod
+    def _shape_from(sv):
+        x0 = sv["front_in"][0]
+        return x0.shape[0], x0.shape[1], x0.shape[2]
+
+    # ----------------------------------------------------------- training head
+    def head_train(self, b6, gt, grads, gscale: float = 1.0, beta: float = 0.0):
+        """Fused: et, MSE(sum) loss, d(et), d(b6 pre-act) (ReLU-masked), head grads. Returns (loss, et, d_b6)."""
+        n, h, w, c = b6.shape
+        if tuple(gt.shape) != (n, 1, h, w):
+            raise ValueError(f"gt shape {tuple(gt.shape)} != {(n, 1, h, w)}")
+        gt = gt.float().contiguous()
+        P = n * h * w
+        et = torch.empty(n, 1, h, w, dtype=torch.float32, device=b6.device)
+        d_b6 = torch.empty_like(b6)
+        nblk = max(1, min(1024, (P * 8 + 255) // 256))
+        part = torch.empty(nblk, 66, dtype=torch.float32, device=b6.device)
+        loss = torch.empty(1, dtype=torch.float32, device=b6.device)
+        self.C.head_train(b6.data_ptr(), self.head.weight.detach().data_ptr(), self.head.bias.detach().data_ptr(),
+                          gt.data_ptr(), et.data_ptr(), d_b6.data_ptr(), part.data_ptr(), nblk,
+                          grads[self.head_w_index].data_ptr(), grads[self.head_b_index].data_ptr(), loss.data_ptr(),
+                          P, float(gscale), float(beta), self._stream())
+        return loss, et, d_b6
+
+    # ----------------------------------------------------------- autograd entry
+    def __call__(self, img: torch.Tensor) -> torch.Tensor:
+        if not torch.is_grad_enabled() or not any(p.requires_grad for p in self._params()):
+            return self.forward_eval(img)
+        return _CANNetFn.apply(img, self, *self._params())
+
+
+class _CANNetFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, img, ex: CANNetExecutor, *params):
+        b6, sv = ex.forward_features(img, save=True)
+        et = ex.head_forward(b6)
+        ctx.ex = ex
+        ctx.sv = sv
+        ctx.b6 = b6
+        return et
+
+    @staticmethod
+    def backward(ctx, g_et):
+        ex: CANNetExecutor = ctx.ex
+        params = ex._params()
+        grads = [torch.empty_like(p, dtype=torch.float32) for p in params]
+        b6 = ctx.b6
+        n, h, w, c = b6.shape
+        g = g_et.float().reshape(n, h, w, 1)
+        b6f = b6.float()
+        hw = ex.head.weight.detach().view(1, c)
+        d_b6 = (g * hw * (b6f > 0)).to(BF16).contiguous()
+        grads[ex.head_w_index].copy_((g * b6f).sum(dim=(0, 1, 2)).view_as(params[ex.head_w_index]))
+        grads[ex.head_b_index].copy_(g.sum().view(1))
+        ex.workspace(*CANNetExecutor._shape_from(ctx.sv))
+        ex.backward_features(ctx.sv, d_b6, grads)
+        ctx.sv = None
+        return (None, None) + tuple(gr.to(p.dtype) for gr, p in zip(grads, params))

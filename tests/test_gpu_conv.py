@@ -66,3 +66,41 @@ def test_conv_dgrad_mask(n, h, w, ci, co, dil):
     (gx,) = torch.autograd.grad(y, xr, dy.float().permute(0, 3, 1, 2))
     ref = gx.permute(0, 2, 3, 1) * (mask.float() > 0)
     _close(dx, ref)
+
+
+@pytest.mark.parametrize("n,h,w,ci,co,k,dil", [
+    (2, 24, 40, 64, 64, 3, 1), (1, 17, 33, 128, 128, 3, 1), (2, 16, 16, 256, 512, 3, 2),
+    (1, 12, 16, 128, 64, 3, 2), (2, 16, 24, 512, 512, 1, 1), (1, 40, 40, 64, 128, 3, 1),
+])
+def test_conv_wgrad(n, h, w, ci, co, k, dil):
+    from can_distributed_pytorch_amd.ops import conv as C
+    torch.manual_seed(3)
+    dev = "cuda"
+    x = torch.randn(n, h, w, ci, device=dev).to(torch.bfloat16)
+    dy = torch.randn(n, h, w, co, device=dev).to(torch.bfloat16)
+    dw = torch.empty(co, ci, k, k, device=dev)
+    db = torch.empty(co, device=dev)
+    C.conv_wgrad(dy, x, dw, db, ksize=k, dil=dil)
+    wr = torch.zeros(co, ci, k, k, device=dev, requires_grad=True)
+    br = torch.zeros(co, device=dev, requires_grad=True)
+    y = F.conv2d(x.float().permute(0, 3, 1, 2), wr, br, padding=dil * (k // 2), dilation=dil)
+    gw, gb = torch.autograd.grad(y, (wr, br), dy.float().permute(0, 3, 1, 2))
+    _close(dw, gw, 1e-2)
+    _close(db, gb, 1e-2)
+
+
+def test_conv_wgrad_first_layer():
+    from can_distributed_pytorch_amd.ops import conv as C
+    torch.manual_seed(4)
+    img = torch.randn(2, 3, 40, 56, device="cuda")
+    x4 = C.to_nhwc4(img)
+    dy = torch.randn(2, 40, 56, 64, device="cuda").to(torch.bfloat16)
+    dw = torch.empty(64, 3, 3, 3, device="cuda")
+    db = torch.empty(64, device="cuda")
+    C.conv_wgrad(dy, x4, dw, db, ksize=3, first=True)
+    wr = torch.zeros(64, 3, 3, 3, device="cuda", requires_grad=True)
+    br = torch.zeros(64, device="cuda", requires_grad=True)
+    y = F.conv2d(x4[..., :3].float().permute(0, 3, 1, 2), wr, br, padding=1)
+    gw, gb = torch.autograd.grad(y, (wr, br), dy.float().permute(0, 3, 1, 2))
+    _close(dw, gw, 1e-2)
+    _close(db, gb, 1e-2)
