@@ -29,6 +29,7 @@
 //   * 1-D grid with a bijective XCD-aware remap so that the channel tiles
 //     sharing one pixel tile (and its halo) run on the same XCD / L2.
 #include "common.h"
+#include "fastdiv.h"
 
 namespace can {
 
@@ -282,6 +283,210 @@ static int dispatch_tiles(const ConvArgs& a, int tile_cfg, hipStream_t s) {
   return -1;
 }
 
+
+// ===========================================================================
+// 8-wave LDS-DMA pipelined variant (every layer except the Cin=3 first one).
+//  * tiles TC x TP = (64*WC) channels x (64*PW*WP) pixels, 8 waves, each
+//    wave 64 ch x 64*PW pix (PW=2: 128 fp32 accumulators per lane);
+//    256x256 for Cout % 256 == 0, 128x256 for Cout % 128, 64x512 for Cout=64;
+//  * global_load_lds_dwordx4 staging (no VGPR round trip), 2 LDS buffers,
+//    the next stage's DMA overlaps the current stage's MFMAs, raw s_barrier
+//    + explicit vmcnt (no __syncthreads vmcnt drain);
+//  * zero padding / tail rows: lanes pointed at a zero page;
+//  * swizzle applied on the DMA source address (LDS image lane-linear).
+// ===========================================================================
+struct ConvArgs2 {
+  const bf16_t* x;
+  const bf16_t* w;
+  const float* bias;
+  const bf16_t* mask;
+  bf16_t* y;
+  const bf16_t* zero;
+  int H, W, Cin, Cout, ksize, dil, M;
+  FastDiv fdW, fdH;
+};
+
+template <int WC, int WP, int PW, int EPI>
+__global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds_kernel(ConvArgs2 a) {
+  constexpr int NW = WC * WP;
+  constexpr int TC = 64 * WC, TP = 64 * PW * WP;
+  constexpr int A_BYTES = TC * 128, B_BYTES = TP * 128;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int NIA = A_BYTES / 1024, NIB = B_BYTES / 1024;
+  constexpr int G = (NIA + NIB) / NW;
+  static_assert((NIA + NIB) % NW == 0, "instruction split");
+
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wave % WC, wp = wave / WC;
+
+  const int nct = a.Cout / TC;
+  const int npt = (a.M + TP - 1) / TP;
+  const int tile = xcd_remap(blockIdx.x, nct * npt);
+  const int ct = tile % nct, pt = tile / nct;
+  const int Ktot = a.ksize * a.ksize * a.Cin;
+  const int cchunks = a.Cin >> 6;
+  const int nk = a.ksize * a.ksize * cchunks;
+
+  auto issue = [&](int ks, int buf) {
+    const int tap = ks / cchunks;
+    const int c0 = (ks - tap * cchunks) * 64;
+    int dh = 0, dw = 0;
+    if (a.ksize == 3) {
+      const int kh = (tap * 11) >> 5;
+      dh = (kh - 1) * a.dil;
+      dw = (tap - kh * 3 - 1) * a.dil;
+    }
+    unsigned char* sbase = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const int gi = wave + NW * i;
+      const void* src = a.zero;
+      unsigned char* dst;
+      if (gi < NIA) {
+        const int r = gi * 8 + (lane >> 3);
+        const int lc = (lane & 7) ^ (r & 7);
+        src = a.w + (size_t)(ct * TC + perm_row(r)) * Ktot + ks * 64 + lc * 8;
+        dst = sbase + gi * 1024;
+      } else {
+        const int r = (gi - NIA) * 8 + (lane >> 3);
+        const int lc = (lane & 7) ^ (r & 7);
+        const int m = pt * TP + r;
+        if (m < a.M) {
+          const uint32_t q = fdiv((uint32_t)m, a.fdW);
+          const int ow = m - (int)q * a.W;
+          const int oh = (int)q - (int)fdiv(q, a.fdH) * a.H;
+          const int ih = oh + dh, iw = ow + dw;
+          if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+            src = a.x + (size_t)(m + dh * a.W + dw) * a.Cin + c0 + lc * 8;
+        }
+        dst = sbase + A_BYTES + (gi - NIA) * 1024;
+      }
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[4][4 * PW];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4 * PW; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  issue(0, 0);
+  for (int ks = 0; ks < nk; ++ks) {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (ks + 1 < nk) issue(ks + 1, (ks + 1) & 1);
+    const uint4* As = reinterpret_cast<const uint4*>(smem + (ks & 1) * STAGE);
+    const uint4* Bs = reinterpret_cast<const uint4*>(smem + (ks & 1) * STAGE + A_BYTES);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = kk * 4 + fq;
+      bf16x8_t af[4], bfr[4 * PW];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = wc * 64 + j * 16 + fr;
+        af[j] = __builtin_bit_cast(bf16x8_t, As[row * 8 + swz(row, chunk)]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4 * PW; ++i) {
+        const int row = wp * 64 * PW + i * 16 + fr;
+        bfr[i] = __builtin_bit_cast(bf16x8_t, Bs[row * 8 + swz(row, chunk)]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4 * PW; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], bfr[i], acc[j][i], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue (same lane ownership as conv_igemm_kernel)
+  const int chb = ct * TC + wc * 64 + fq * 16;
+  float bias[16];
+  if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS) {
+#pragma unroll
+    for (int c = 0; c < 16; c += 4) {
+      const float4 b4 = *reinterpret_cast<const float4*>(a.bias + chb + c);
+      bias[c] = b4.x; bias[c + 1] = b4.y; bias[c + 2] = b4.z; bias[c + 3] = b4.w;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4 * PW; ++i) {
+    const int m = pt * TP + wp * 64 * PW + i * 16 + fr;
+    if (m >= a.M) continue;
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[j * 4 + r] = acc[j][i][r];
+    if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        v[c] += bias[c];
+        if (EPI == EPI_BIAS_RELU) v[c] = fmaxf(v[c], 0.f);
+      }
+    }
+    if (EPI == EPI_SIGMOID) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) v[c] = 1.f / (1.f + __expf(-v[c]));
+    }
+    const size_t off = (size_t)m * a.Cout + chb;
+    if (EPI == EPI_MASK) {
+      const uint4 m0 = *reinterpret_cast<const uint4*>(a.mask + off);
+      const uint4 m1 = *reinterpret_cast<const uint4*>(a.mask + off + 8);
+      const unsigned mw[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const unsigned short bits = (unsigned short)(mw[c >> 1] >> ((c & 1) * 16));
+        const bool pos = ((bits & 0x8000u) == 0) && ((bits & 0x7fffu) != 0);
+        v[c] = pos ? v[c] : 0.f;
+      }
+    }
+    *reinterpret_cast<uint4*>(a.y + off) =
+        make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
+    *reinterpret_cast<uint4*>(a.y + off + 8) =
+        make_uint4(pack2bf(v[8], v[9]), pack2bf(v[10], v[11]), pack2bf(v[12], v[13]), pack2bf(v[14], v[15]));
+  }
+}
+
+template <int WC, int WP, int PW, int EPI>
+static int launch_glds(const ConvArgs2& a, hipStream_t s) {
+  constexpr int TC = 64 * WC, TP = 64 * PW * WP;
+  const size_t lds = 2 * (size_t)(TC + TP) * 128;
+  auto kfn = conv_glds_kernel<WC, WP, PW, EPI>;
+  static bool attr = false;
+  if (!attr) {
+    CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  const int nct = a.Cout / TC, npt = (a.M + TP - 1) / TP;
+  hipLaunchKernelGGL(kfn, dim3(nct * npt), dim3(64 * WC * WP), lds, s, a);
+  return (int)hipGetLastError();
+}
+
+template <int EPI>
+static int dispatch_glds(const ConvArgs2& a, int tile_cfg, hipStream_t s) {
+  int cfg = tile_cfg;
+  if (cfg == 0) cfg = (a.Cout % 256 == 0) ? 11 : (a.Cout % 128 == 0) ? 12 : 13;
+  switch (cfg) {
+    case 11: if (a.Cout % 256) return -8; return launch_glds<4, 2, 2, EPI>(a, s);
+    case 12: if (a.Cout % 128) return -8; return launch_glds<2, 4, 1, EPI>(a, s);
+    case 13: return launch_glds<1, 8, 1, EPI>(a, s);
+  }
+  return -9;
+}
+
+static const bf16_t* conv_zero_page() {
+  static void* z = nullptr;
+  if (!z) {
+    if (hipMalloc(&z, 4096) != hipSuccess) return nullptr;
+    if (hipMemset(z, 0, 4096) != hipSuccess) return nullptr;
+  }
+  return (const bf16_t*)z;
+}
+
 }  // namespace can
 
 extern "C" int can_conv_igemm(const void* x, const void* w, const float* bias, const void* mask, void* y,
@@ -301,6 +506,22 @@ extern "C" int can_conv_igemm(const void* x, const void* w, const float* bias, c
   if (first) {
     CAN_EPI_CASE(LOAD_FIRST, EPI_BIAS_RELU)
     return -5;
+  }
+  if (tile_cfg == 0 || tile_cfg >= 10) {
+    if (H < 2 || W < 2) return -7;
+    ConvArgs2 b;
+    b.x = a.x; b.w = a.w; b.bias = a.bias; b.mask = a.mask; b.y = a.y; b.zero = conv_zero_page();
+    if (!b.zero) return -10;
+    b.H = H; b.W = W; b.Cin = Cin; b.Cout = Cout; b.ksize = ksize; b.dil = dil; b.M = a.M;
+    b.fdW = make_fastdiv((uint32_t)W); b.fdH = make_fastdiv((uint32_t)H);
+    switch (epi) {
+      case EPI_BIAS_RELU: return dispatch_glds<EPI_BIAS_RELU>(b, tile_cfg, s);
+      case EPI_MASK: return dispatch_glds<EPI_MASK>(b, tile_cfg, s);
+      case EPI_NONE: return dispatch_glds<EPI_NONE>(b, tile_cfg, s);
+      case EPI_BIAS: return dispatch_glds<EPI_BIAS>(b, tile_cfg, s);
+      case EPI_SIGMOID: return dispatch_glds<EPI_SIGMOID>(b, tile_cfg, s);
+    }
+    return -6;
   }
   CAN_EPI_CASE(LOAD_GENERIC, EPI_BIAS_RELU)
   CAN_EPI_CASE(LOAD_GENERIC, EPI_MASK)

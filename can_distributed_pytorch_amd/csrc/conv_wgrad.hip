@@ -28,6 +28,7 @@
 //   <1,1,4>: 64 co x 64 k tile, 128-pixel stages, each wave a 32-pixel quarter
 //            of every stage; the 4 partial tiles are summed through LDS.
 #include "common.h"
+#include "fastdiv.h"
 
 namespace can {
 
@@ -209,19 +210,12 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], bfr[i], acc[j][i], 0, 0, 0);
-      if (do_bias) {
-        if (WM == 1) {
-          // wave (wc, wk) sums co tiles {2wk, 2wk+1}
+      // bias gradient: sum over pixels = MFMA against a ones operand.  Static
+      // indices only (a runtime-indexed accumulator array spills to VGPR copies).
+      if (do_bias && (WM != 1 || wk == 0)) {
 #pragma unroll
-          for (int jj = 0; jj < 2; ++jj) {
-            const int j = 2 * wk + jj;
-            accb[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], ones, accb[j], 0, 0, 0);
-          }
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            accb[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], ones, accb[j], 0, 0, 0);
-        }
+        for (int j = 0; j < 4; ++j)
+          accb[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], ones, accb[j], 0, 0, 0);
       }
     }
     if (st + 1 < nstage) store_stage(buf ^ 1);
@@ -240,10 +234,9 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
         const int co = co0 + wc * 64 + j * 16 + fq * 4;
         *reinterpret_cast<f32x4*>(slab + (size_t)k * a.Cout + co) = acc[j][i];
       }
-    if (do_bias && fr == 0) {
+    if (do_bias && wk == 0 && fr == 0) {
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        const int j = 2 * wk + jj;
+      for (int j = 0; j < 4; ++j) {
         const int co = co0 + wc * 64 + j * 16 + fq * 4;
         *reinterpret_cast<f32x4*>(a.wsb + (size_t)slice * a.Cout + co) = accb[j];
       }
@@ -281,6 +274,262 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
       *reinterpret_cast<f32x4*>(a.wsb + (size_t)slice * a.Cout + co) = s;
     }
   }
+}
+
+// ===========================================================================
+// LDS-DMA pipelined variant (all layers except the Cin=3 first layer).
+//
+// Same math and output as conv_wgrad_kernel, restructured for latency:
+//  * both tiles are staged by global_load_lds_dwordx4 (LDS-DMA, no VGPR
+//    round trip); zero padding = lanes pointed at a zero page;
+//  * NBUF-deep ring of stages, NBUF-1 stages in flight, counted
+//    s_waitcnt vmcnt(N) + raw s_barrier (never a vmcnt(0) drain in the loop);
+//  * the swizzle that makes the transposed reads conflict-free is applied to
+//    the per-lane SOURCE address (the LDS destination of an LDS-DMA is
+//    lane-linear), and the same XOR is used on the read side;
+//  * k tiles may straddle taps (Cin = 64 layers): each 16-B chunk computes
+//    its own (tap, ci); k >= K chunks read zeros and are not stored;
+//  * pixel -> (oh, ow) by multiply-high division (no integer divide).
+// Waves: WC x WK x WM, each 64 co x 64 k over 64 pixels of every stage
+// (WM > 1: the waves split the stage's pixels, partial tiles summed in LDS).
+// ===========================================================================
+struct WgradArgs2 {
+  const bf16_t* dy;
+  const bf16_t* x;
+  const bf16_t* zero;   // >= 16 B of zeros
+  float* ws;
+  float* wsb;
+  int H, W, Cin, Cout, ksize, dil, M, K, S, mslice;
+  FastDiv fdW, fdH, fdC;
+};
+
+template <int RB>   // row bytes
+__device__ __forceinline__ int swz8b(int row, int c8) {
+  if (RB >= 256) return c8 ^ (((row & 3) | (((row >> 3) & 1) << 2)) << 2);
+  else return c8 ^ (((((row >> 1) & 1)) | (((row >> 3) & 1) << 1)) << 2);
+}
+
+template <int WC, int WK, int WM, int NBUF>
+__global__ void __launch_bounds__(64 * WC * WK * WM, (WC * WK * WM >= 8) ? 1 : 2) wgrad_glds_kernel(WgradArgs2 a) {
+  constexpr int NW = WC * WK * WM;
+  constexpr int TCo = 64 * WC, TK = 64 * WK;
+  constexpr int BKM = 64 * WM;
+  constexpr int RBA = TCo * 2, RBB = TK * 2;
+  constexpr int A_BYTES = BKM * RBA, B_BYTES = BKM * RBB;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int NIA = A_BYTES / 1024, NIB = B_BYTES / 1024;
+  constexpr int G = (NIA + NIB) / NW;            // LDS-DMA instructions per wave per stage
+  static_assert((NIA + NIB) % NW == 0, "instruction split");
+  constexpr int D = NBUF - 1;                     // stages in flight
+
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wave % WC, wk = (wave / WC) % WK, wm = wave / (WC * WK);
+
+  const int nco = a.Cout / TCo, nkt = (a.K + TK - 1) / TK;
+  const int ntile = nco * nkt;
+  const int bid = xcd_remap(blockIdx.x, ntile * a.S);
+  const int tile = bid % ntile, slice = bid / ntile;
+  const int co0 = (tile % nco) * TCo, k0 = (tile / nco) * TK;
+  const bool do_bias = (a.wsb != nullptr) && (k0 == 0);
+  const int mbeg = slice * a.mslice;
+  const int mend = min(a.M, mbeg + a.mslice);
+  const int nstage = (mend > mbeg) ? (mend - mbeg + BKM - 1) / BKM : 0;
+
+  // ---- LDS-DMA issue of one stage.  Per-lane source addresses are
+  // recomputed from (wave, instruction, lane) each time: keeping G
+  // descriptors live would cost ~40 VGPRs and push the accumulators out of
+  // the AGPR file (hipcc then copies them around every MFMA).
+  auto issue = [&](int st, int buf) {
+    const int m0 = mbeg + st * BKM;
+    unsigned char* sbase = smem + buf * STAGE;
+    int lane = tid & 63;
+    // small tiles issue many LDS-DMA per stage: keep the compiler from
+    // hoisting G address sets out of the loop (they would spill)
+    if constexpr (G > 8) asm volatile("" : "+v"(lane));
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const int gi = wave + NW * i;          // wave-uniform
+      const void* src = a.zero;
+      unsigned char* dst;
+      if (gi < NIA) {
+        const int byte = gi * 1024 + lane * 16;
+        const int row = byte / RBA;
+        const int lc16 = swz8b<RBA>(row, ((byte % RBA) / 16) * 2) >> 1;
+        const int m = m0 + row;
+        if (m < mend) src = a.dy + (size_t)m * a.Cout + co0 + lc16 * 8;
+        dst = sbase + gi * 1024;
+      } else {
+        const int byte = (gi - NIA) * 1024 + lane * 16;
+        const int row = byte / RBB;
+        const int lc16 = swz8b<RBB>(row, ((byte % RBB) / 16) * 2) >> 1;
+        const int m = m0 + row;
+        const int k = k0 + lc16 * 8;
+        if (k < a.K && m < mend) {
+          const int tap = (int)fdiv((uint32_t)k, a.fdC);
+          const int ci = k - tap * a.Cin;
+          int dh = 0, dw = 0;
+          if (a.ksize == 3) {
+            const int kh = (tap * 11) >> 5;        // tap / 3 for tap < 9
+            dh = (kh - 1) * a.dil;
+            dw = (tap - kh * 3 - 1) * a.dil;
+          }
+          const uint32_t qq = fdiv((uint32_t)m, a.fdW);
+          const int ow = m - (int)qq * a.W;
+          const int oh = (int)qq - (int)fdiv(qq, a.fdH) * a.H;
+          const int ih = oh + dh, iw = ow + dw;
+          if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+            src = a.x + (size_t)(m + dh * a.W + dw) * a.Cin + ci;
+        }
+        dst = sbase + A_BYTES + (gi - NIA) * 1024;
+      }
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[4][4];
+  f32x4 accb[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    accb[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  bf16x8_t ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  auto rd = [&](const unsigned char* base, int rb_is_wide, int rb, int prow0, int col0) -> bf16x8_t {
+    const int r0 = prow0 + 8 * g + q;
+    const int c8 = (col0 >> 2) + p;
+    const int s0 = rb_is_wide ? swz8b<256>(r0, c8) : swz8b<128>(r0, c8);
+    const int s1 = rb_is_wide ? swz8b<256>(r0 + 4, c8) : swz8b<128>(r0 + 4, c8);
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + r0 * rb + s0 * 8));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + (r0 + 4) * rb + s1 * 8));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8_t, v);
+  };
+
+  // prologue: D stages in flight
+#pragma unroll
+  for (int s = 0; s < D; ++s)
+    if (s < nstage) issue(s, s);
+
+  for (int st = 0; st < nstage; ++st) {
+    if (nstage - 1 - st >= D - 1) {
+      if constexpr (D >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * G) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (st + D < nstage) issue(st + D, (st + D) % NBUF);
+    const unsigned char* Ab = smem + (st % NBUF) * STAGE;
+    const unsigned char* Bb = Ab + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int prow0 = wm * 64 + kk * 32;
+      bf16x8_t af[4], bfr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) af[j] = rd(Ab, RBA >= 256, RBA, prow0, wc * 64 + j * 16);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bfr[i] = rd(Bb, RBB >= 256, RBB, prow0, wk * 64 + i * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], bfr[i], acc[j][i], 0, 0, 0);
+      if (do_bias && wk == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) accb[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], ones, accb[j], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- epilogue
+  const int fr = lane & 15, fq = lane >> 4;
+  float* slab = a.ws + (size_t)slice * a.K * a.Cout;
+  if (WM == 1) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = k0 + wk * 64 + i * 16 + fr;
+        const int co = co0 + wc * 64 + j * 16 + fq * 4;
+        if (k < a.K) *reinterpret_cast<f32x4*>(slab + (size_t)k * a.Cout + co) = acc[j][i];
+      }
+    if (do_bias && wk == 0 && fr == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int co = co0 + wc * 64 + j * 16 + fq * 4;
+        *reinterpret_cast<f32x4*>(a.wsb + (size_t)slice * a.Cout + co) = accb[j];
+      }
+    }
+  } else {
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);   // [NW][16][64][4] (+ bias [NW][4][64][4])
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        *reinterpret_cast<f32x4*>(red + ((wave * 16 + j * 4 + i) * 64 + lane) * 4) = acc[j][i];
+    float* redb = red + NW * 16 * 64 * 4;
+    if (do_bias) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) *reinterpret_cast<f32x4*>(redb + ((wave * 4 + j) * 64 + lane) * 4) = accb[j];
+    }
+    __syncthreads();
+    if (wm == 0) {
+      // waves of the first pixel group reduce and store their own (wc, wk) tile
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int w2 = 0; w2 < WM; ++w2) {
+            const int wv = wave + w2 * WC * WK;
+            s += *reinterpret_cast<const f32x4*>(red + ((wv * 16 + j * 4 + i) * 64 + lane) * 4);
+          }
+          const int k = k0 + wk * 64 + i * 16 + fr;
+          const int co = co0 + wc * 64 + j * 16 + fq * 4;
+          if (k < a.K) *reinterpret_cast<f32x4*>(slab + (size_t)k * a.Cout + co) = s;
+        }
+      if (do_bias && wk == 0 && fr == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int w2 = 0; w2 < WM; ++w2) {
+            const int wv = wave + w2 * WC * WK;
+            s += *reinterpret_cast<const f32x4*>(redb + ((wv * 4 + j) * 64 + lane) * 4);
+          }
+          const int co = co0 + wc * 64 + j * 16 + fq * 4;
+          *reinterpret_cast<f32x4*>(a.wsb + (size_t)slice * a.Cout + co) = s;
+        }
+      }
+    }
+  }
+}
+
+template <int WC, int WK, int WM, int NBUF>
+static int launch_wgrad2(const WgradArgs2& a, hipStream_t s) {
+  constexpr int NW = WC * WK * WM;
+  constexpr int STAGE = 64 * WM * (64 * WC + 64 * WK) * 2;
+  size_t lds = (size_t)NBUF * STAGE;
+  if (WM > 1) lds = std::max(lds, (size_t)(NW * 16 * 64 * 4 + NW * 4 * 64 * 4) * 4);
+  auto kfn = wgrad_glds_kernel<WC, WK, WM, NBUF>;
+  static bool attr = false;
+  if (!attr) {
+    CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  const int ntile = (a.Cout / (64 * WC)) * ((a.K + 64 * WK - 1) / (64 * WK));
+  hipLaunchKernelGGL(kfn, dim3(ntile * a.S), dim3(64 * NW), lds, s, a);
+  return (int)hipGetLastError();
 }
 
 // Sum S slabs [S][Ktot][Cout] in fixed order and write dW in the PyTorch
@@ -335,15 +584,32 @@ static int launch_wgrad(const WgradArgs& a, hipStream_t s) {
 
 }  // namespace can
 
-// Workspace needed (floats) for a given split; the Python side sizes one
-// shared workspace for the largest layer.
+// Tile configs of the pipelined kernel: 1 = 128co x 128k (4 waves, 4 bufs),
+// 2 = 256co x 128k (8 waves, 3 bufs), 3 = 64co x 128k (4 waves, pixel-split 2,
+// 3 bufs), 4 = 64co x 64k (2 waves, pixel-split 2, 4 bufs); 0 = first layer
+// (register-staged kernel).
+static void wgrad_tile(int cfg, int* TCo, int* TK, int* BKM) {
+  switch (cfg) {
+    case 1: *TCo = 128; *TK = 128; *BKM = 64; break;
+    case 2: *TCo = 256; *TK = 128; *BKM = 64; break;
+    case 3: *TCo = 64; *TK = 128; *BKM = 128; break;
+    case 4: *TCo = 64; *TK = 64; *BKM = 128; break;
+    default: *TCo = 64; *TK = 64; *BKM = 128; break;
+  }
+}
+
 extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, int target_blocks, int* S_out,
                               int* mslice_out, int* cfg_out) {
-  const int Ktot = first ? 64 : ksize * ksize * Cin;
-  const int cfg = (!first && Cout % 128 == 0 && Cin % 128 == 0) ? 1 : 2;
-  const int TCo = cfg == 1 ? 128 : 64, TK = cfg == 1 ? 128 : 64;
-  const int BKM = cfg == 1 ? 64 : 128;
-  const int ntile = (Cout / TCo) * (Ktot / TK);
+  const int K = first ? 64 : ksize * ksize * Cin;
+  int cfg;
+  if (first) cfg = 0;
+  else if (Cout % 256 == 0 && K >= 1024) cfg = 2;
+  else if (Cout % 128 == 0) cfg = 1;
+  else if (K >= 128) cfg = 3;
+  else cfg = 4;
+  int TCo, TK, BKM;
+  wgrad_tile(cfg, &TCo, &TK, &BKM);
+  const int ntile = (Cout / TCo) * ((K + TK - 1) / TK);
   int S = (target_blocks + ntile - 1) / ntile;
   const int max_s = (M + BKM - 1) / BKM;
   if (S > max_s) S = max_s;
@@ -355,29 +621,49 @@ extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, in
   return 0;
 }
 
+static const can::bf16_t* zero_page() {
+  static void* z = nullptr;
+  if (!z) {
+    if (hipMalloc(&z, 4096) != hipSuccess) return nullptr;
+    if (hipMemset(z, 0, 4096) != hipSuccess) return nullptr;
+  }
+  return (const can::bf16_t*)z;
+}
+
 extern "C" int can_conv_wgrad(const void* dy, const void* x, float* ws, float* wsb, float* dw, float* db, int N,
                               int H, int W, int Cin, int Cout, int ksize, int dil, int first, int S, int mslice,
                               int cfg, float beta, float scale, void* stream) {
   using namespace can;
-  WgradArgs a;
-  a.dy = (const bf16_t*)dy; a.x = (const bf16_t*)x; a.ws = ws; a.wsb = (db != nullptr) ? wsb : nullptr;
-  a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.ksize = ksize; a.dil = dil; a.M = N * H * W;
-  a.Ktot = first ? 64 : ksize * ksize * Cin; a.S = S; a.mslice = mslice;
   hipStream_t s = (hipStream_t)stream;
+  const int K = first ? 64 : ksize * ksize * Cin;
+  float* wsb_used = (db != nullptr) ? wsb : nullptr;
   int rc;
-  if (first) {
+  if (first || cfg == 0) {
     if (Cin != 4 || Cout % 64) return -2;
+    WgradArgs a;
+    a.dy = (const bf16_t*)dy; a.x = (const bf16_t*)x; a.ws = ws; a.wsb = wsb_used;
+    a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.ksize = ksize; a.dil = dil; a.M = N * H * W;
+    a.Ktot = 64; a.S = S; a.mslice = mslice;
     rc = launch_wgrad<1, 1, 4, true>(a, s);
-  } else if (cfg == 1) {
-    if (Cout % 128 || Cin % 128) return -3;
-    rc = launch_wgrad<2, 2, 1, false>(a, s);
   } else {
-    if (Cout % 64 || Cin % 64) return -4;
-    rc = launch_wgrad<1, 1, 4, false>(a, s);
+    if (Cin % 64 || Cout % 64 || H < 2 || W < 2) return -3;
+    WgradArgs2 a;
+    a.dy = (const bf16_t*)dy; a.x = (const bf16_t*)x; a.zero = zero_page(); a.ws = ws; a.wsb = wsb_used;
+    if (!a.zero) return -7;
+    a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.ksize = ksize; a.dil = dil; a.M = N * H * W; a.K = K;
+    a.S = S; a.mslice = mslice;
+    a.fdW = make_fastdiv((uint32_t)W); a.fdH = make_fastdiv((uint32_t)H); a.fdC = make_fastdiv((uint32_t)Cin);
+    switch (cfg) {
+      case 1: if (Cout % 128) return -4; rc = launch_wgrad2<2, 2, 1, 4>(a, s); break;
+      case 2: if (Cout % 256) return -4; rc = launch_wgrad2<4, 2, 1, 3>(a, s); break;
+      case 3: rc = launch_wgrad2<1, 2, 2, 3>(a, s); break;
+      case 4: rc = launch_wgrad2<1, 1, 2, 4>(a, s); break;
+      default: return -5;
+    }
   }
   if (rc) return rc;
-  const int plane = a.Ktot * Cout;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((plane + 255) / 256), dim3(256), 0, s, ws, a.wsb, dw, db, S, a.Ktot,
+  const int plane = K * Cout;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((plane + 255) / 256), dim3(256), 0, s, ws, wsb_used, dw, db, S, K,
                      Cout, first ? 4 : Cin, ksize * ksize, first, beta, scale);
   return (int)hipGetLastError();
 }

@@ -26,6 +26,8 @@ def _close(a, b, tol=2e-2):
     (1, 12, 16, 1024, 512, 3, 2, 0), (2, 16, 24, 512, 512, 1, 1, 0),
     (1, 20, 20, 128, 256, 3, 1, 1), (1, 20, 20, 128, 256, 3, 1, 2), (1, 20, 20, 128, 256, 3, 1, 3),
     (1, 20, 20, 128, 256, 3, 1, 4),
+    (1, 20, 20, 128, 256, 3, 1, 11), (1, 20, 20, 128, 256, 3, 1, 12), (1, 20, 20, 128, 256, 3, 1, 13),
+    (2, 9, 13, 64, 128, 3, 2, 0), (1, 7, 5, 512, 1024, 3, 2, 0), (3, 11, 17, 64, 64, 3, 1, 0),
 ])
 def test_conv_fwd(n, h, w, ci, co, k, dil, tile):
     from can_distributed_pytorch_amd.ops import conv as C
@@ -71,6 +73,7 @@ def test_conv_dgrad_mask(n, h, w, ci, co, dil):
 @pytest.mark.parametrize("n,h,w,ci,co,k,dil", [
     (2, 24, 40, 64, 64, 3, 1), (1, 17, 33, 128, 128, 3, 1), (2, 16, 16, 256, 512, 3, 2),
     (1, 12, 16, 128, 64, 3, 2), (2, 16, 24, 512, 512, 1, 1), (1, 40, 40, 64, 128, 3, 1),
+    (1, 7, 9, 256, 256, 3, 2), (2, 13, 11, 64, 64, 3, 1), (1, 9, 10, 1024, 512, 3, 2), (1, 6, 8, 128, 256, 3, 1),
 ])
 def test_conv_wgrad(n, h, w, ci, co, k, dil):
     from can_distributed_pytorch_amd.ops import conv as C
