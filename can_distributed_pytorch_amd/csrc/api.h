@@ -36,6 +36,9 @@ int can_ctx_bwd_e1(const void* dcat, const void* ws, const float* T, void* dz, v
 int can_ctx_bwd_final(const void* dcat, const void* dc, const float* dave, const void* fv, void* dfv, int N, int h,
                       int w, int C, void* stream);
 
+// density.hip
+int can_density_map(const float* pts, int n, int H, int W, float* sigma_ws, float* out, int max_r, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -14,6 +14,8 @@
 
 namespace py = pybind11;
 
+void register_rccl(py::module_& m);   // rccl_reducer.cpp
+
 static void check(int rc, const char* what) {
   if (rc != 0) {
     std::string msg = std::string(what) + " failed: rc=" + std::to_string(rc);
@@ -26,6 +28,7 @@ static void check(int rc, const char* what) {
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "gfx950 native kernels and runtime for can_distributed_pytorch_amd";
+  register_rccl(m);
 
   m.def("arch", []() {
     int dev = 0;
@@ -103,5 +106,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("ctx_bwd_final", [](uintptr_t dcat, uintptr_t dc, uintptr_t dave, uintptr_t fv, uintptr_t dfv, int N, int h,
                             int w, int C, uintptr_t st) {
     check(can_ctx_bwd_final(P(dcat), P(dc), (const float*)dave, P(fv), P(dfv), N, h, w, C, P(st)), "ctx_bwd_final");
+  });
+  // ---- density maps
+  m.def("density_map", [](uintptr_t pts, int n, int H, int W, uintptr_t sig, uintptr_t out, int max_r, uintptr_t st) {
+    check(can_density_map((const float*)pts, n, H, W, (float*)sig, (float*)out, max_r, P(st)), "density_map");
   });
 }

@@ -1,0 +1,86 @@
+"""CrowdDataset — reference data contract (model/CrowdDataset.py:11-69).
+
+``CrowdDataset(img_root, gt_dmap_root, gt_downsample=1, phase='train')``
+lists the files of ``img_root``; item i = (image [3,H',W'] float32 ImageNet-
+normalised, density [1,H'/d,W'/d] float32) with H', W' the largest multiples
+of d, a random horizontal flip of BOTH in phase 'train', and the ground
+truth loaded from ``gt_dmap_root/<name>.npy`` (``.jpg`` -> ``.npy``).
+
+Differences: gt_downsample <= 1 works (Q8), integer
+images only are /255 (Q14), decoding uses PIL (cv2 is not a dependency),
+the flip RNG is seedable.  ``SyntheticCrowdDataset`` provides the same item
+contract without files (benchmarks, tests, smoke runs).
+"""
+from __future__ import annotations
+
+import os
+import random
+from typing import Optional
+
+import numpy as np
+import torch
+from torch.utils.data import Dataset
+
+from .transforms import prepare_pair
+
+IMG_EXT = (".jpg", ".jpeg", ".png", ".bmp", ".tif", ".tiff")
+
+
+def imread(path: str) -> np.ndarray:
+    from PIL import Image
+    with Image.open(path) as im:
+        if im.mode not in ("L", "RGB", "RGBA"):
+            im = im.convert("RGB")
+        return np.asarray(im)
+
+
+class CrowdDataset(Dataset):
+    def __init__(self, img_root: str, gt_dmap_root: str, gt_downsample: int = 1, phase: str = "train",
+                 seed: Optional[int] = None):
+        self.img_root = img_root
+        self.gt_dmap_root = gt_dmap_root
+        self.gt_downsample = max(1, int(gt_downsample))
+        self.phase = phase
+        self.img_names = sorted(f for f in os.listdir(img_root)
+                                if os.path.isfile(os.path.join(img_root, f)) and f.lower().endswith(IMG_EXT))
+        self.n_samples = len(self.img_names)
+        self._rng = random.Random(seed)
+
+    def __len__(self):
+        return self.n_samples
+
+    def gt_path(self, name: str) -> str:
+        stem = os.path.splitext(name)[0]
+        return os.path.join(self.gt_dmap_root, stem + ".npy")
+
+    def __getitem__(self, index):
+        if not 0 <= index < len(self):
+            raise IndexError("index range error")
+        name = self.img_names[index]
+        img = imread(os.path.join(self.img_root, name))
+        dmap = np.load(self.gt_path(name))                       # allow_pickle=False (default)
+        flip = self.phase == "train" and self._rng.randint(0, 1) == 1
+        im, dm = prepare_pair(img, dmap, self.gt_downsample, flip)
+        return torch.from_numpy(np.ascontiguousarray(im)), torch.from_numpy(np.ascontiguousarray(dm))
+
+
+class SyntheticCrowdDataset(Dataset):
+    """Deterministic synthetic crowd images of a fixed size (same item contract)."""
+
+    def __init__(self, n: int, height: int = 768, width: int = 1024, gt_downsample: int = 8, seed: int = 0,
+                 heads=(100, 1500)):
+        from .synthetic import make_synthetic_batch
+        self._make = make_synthetic_batch
+        self.n, self.h, self.w = n, height, width
+        self.seed = seed
+        self.heads = heads
+        self.gt_downsample = gt_downsample
+        if gt_downsample != 8:
+            raise ValueError("synthetic density maps are produced at 1/8 resolution")
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, index):
+        img, gt = self._make(1, self.h, self.w, seed=self.seed * 100003 + index, heads=self.heads)
+        return img[0], gt[0]

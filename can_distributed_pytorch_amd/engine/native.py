@@ -45,11 +45,12 @@ class NativeStepper:
         self.lr = lr * world                       # train.py:25 linear scaling
         self.momentum = momentum
         self.params = list(self.model.parameters())
-        self.arena = FlatArena(self.params, self.device)
-        self.mom = torch.zeros_like(self.arena.data)  # momentum buffer (zero init == torch's first-step clone)
-        self.grads = self.arena.grad_views()
         self.ex = CANNetExecutor(self.model)
         self.model._executor = self.ex
+        # fp32 master/grad arenas laid out in gradient-ready order (contiguous buckets)
+        self.arena = FlatArena(self.params, self.device, order=self.ex.grad_ready_order())
+        self.mom = torch.zeros_like(self.arena.data)  # momentum buffer (zero init == torch's first-step clone)
+        self.grads = self.arena.grad_views()
         self.flags = torch.zeros(4, dtype=torch.float32, device=self.device)   # [nonfinite, loss, ...]
         self.reducer = reducer
         if self.reducer is None and world > 1:
@@ -67,7 +68,10 @@ class NativeStepper:
     # ------------------------------------------------------------ helpers
     def _broadcast_params(self):
         """Init-time consistency (train.py:98-114 + DDP ctor broadcast) in ONE collective."""
-        dist.broadcast(self.arena.data, src=0)
+        if self.reducer is not None:
+            self.reducer.broadcast_arena(0)
+        else:
+            dist.broadcast(self.arena.data, src=0)
         self.ex.refresh_packs(force=True)
 
     def _step_body(self, img, gt, update: bool = True):

@@ -85,6 +85,17 @@ class CANNetExecutor:
         self.ws = None
         self.stream_override = None
 
+    def grad_ready_order(self) -> List[int]:
+        """Parameter indices in the order backward_features produces them."""
+        order = [self.head_w_index, self.head_b_index]
+        for s in reversed(self.back):
+            order += [s.w_index, s.b_index]
+        order += [self.ctx2_index[sc] for sc in CONTEXT_SCALES]
+        order += [self.ctx1_index[sc] for sc in CONTEXT_SCALES]
+        for s in reversed(self.front):
+            order += [s.w_index, s.b_index]
+        return order
+
     # ----------------------------------------------------------- weights
     def _params(self):
         return list(self.model.parameters())
@@ -262,8 +273,28 @@ class CANNetExecutor:
             else:
                 dcat = C.conv_igemm(dy, dgr, None, ksize=3, dil=s.dil, epi=C.EPI_NONE)
         # ---- context module
-        fv = sv["fv"]
-        ctx = sv["ctx"]
+        dy = self._context_bwd(sv["ctx"], sv["fv"], dcat, grads, ws, beta, scale, ready)
+        # ---- frontend, reverse
+        for s in reversed(self.front):
+            x = sv["front_in"][s.idx]
+            wg(s, dy, x, 3, 1, s.first, s.w_index, s.b_index)
+            if s.idx == 0:
+                break
+            _, dgr = self.packs[id(s.module.weight)]
+            prev = self.front[s.idx - 1]
+            if prev.pool_after:
+                dp = C.conv_igemm(dy, dgr, None, ksize=3, dil=1, epi=C.EPI_NONE)
+                full = sv["pre_pool"][prev.idx]
+                dfull = torch.empty_like(full)
+                nn_, hh, ww, cc = full.shape
+                self.C.maxpool_bwd_relu(full.data_ptr(), dp.data_ptr(), dfull.data_ptr(), nn_, hh, ww, cc, st)
+                dy = dfull
+            else:
+                dy = C.conv_igemm(dy, dgr, None, ksize=3, dil=1, epi=C.EPI_MASK, mask=x)
+
+    def _context_bwd(self, ctx, fv, dcat, grads, ws, beta, scale, ready):
+        """Backward of the context module; returns d(F10 pre-activation) (ReLU mask of fv applied)."""
+        st = self._stream()
         n, h, w, c = fv.shape
         dz = torch.empty(4, n, h, w, c, dtype=BF16, device=fv.device)
         sdir = torch.empty_like(dz)
@@ -298,24 +329,7 @@ class CANNetExecutor:
         dfv = torch.empty(n, h, w, c, dtype=BF16, device=fv.device)
         self.C.ctx_bwd_final(dcat.data_ptr(), dc.data_ptr(), dave.data_ptr(), fv.data_ptr(), dfv.data_ptr(), n, h, w,
                              c, st)
-        # ---- frontend, reverse
-        dy = dfv
-        for s in reversed(self.front):
-            x = sv["front_in"][s.idx]
-            wg(s, dy, x, 3, 1, s.first, s.w_index, s.b_index)
-            if s.idx == 0:
-                break
-            _, dgr = self.packs[id(s.module.weight)]
-            prev = self.front[s.idx - 1]
-            if prev.pool_after:
-                dp = C.conv_igemm(dy, dgr, None, ksize=3, dil=1, epi=C.EPI_NONE)
-                full = sv["pre_pool"][prev.idx]
-                dfull = torch.empty_like(full)
-                nn_, hh, ww, cc = full.shape
-                self.C.maxpool_bwd_relu(full.data_ptr(), dp.data_ptr(), dfull.data_ptr(), nn_, hh, ww, cc, st)
-                dy = dfull
-            else:
-                dy = C.conv_igemm(dy, dgr, None, ksize=3, dil=1, epi=C.EPI_MASK, mask=x)
+        return dfv
 
     @staticmethod
     def _shape_from(sv):

@@ -1,0 +1,183 @@
+"""Bucketed gradient reducer (this framework's DistributedDataParallel).
+
+Reference: torch DDP as used at train.py:121-122 (1 MiB first
+bucket, 25 MiB buckets, built in gradient-ready order, all-reduce overlapped
+with backward, averaged by world size).  Re-designed for MI355X:
+
+* the fp32 gradient arena (utils/flat.py) is laid out in gradient-READY
+  order, so each bucket is one contiguous slice and the all-reduce runs in
+  place — no copy-in / copy-out;
+* ``mark_ready(param_indices)`` is called by the native executor right after
+  a layer's weight-gradient kernel (or by post-accumulate-grad hooks on the
+  autograd path); when a bucket is complete it is launched — strictly in
+  bucket order so that every rank issues identical collective sequences;
+* transport "rccl": the C++ BucketReducer (csrc/rccl_reducer.cpp) — own
+  RCCL communicator, comm stream at high priority, one hipEvent per bucket,
+  graph-capturable;  transport "torch": torch.distributed (gloo on CPU for the
+  fake-cluster tests, or NCCL) with async work handles;
+* averaging (1/world) is folded into the fused SGD kernel, not done here.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from ..utils.flat import FlatArena
+
+MIB = 1 << 20
+
+
+@dataclass
+class Bucket:
+    start: int          # element offset into the arena
+    end: int
+    params: List[int]   # parameter indices (model.parameters() order)
+
+    @property
+    def numel(self):
+        return self.end - self.start
+
+
+def plan_buckets(arena: FlatArena, ready_order: Sequence[int], bucket_mb: float = 25.0,
+                 first_bucket_mb: float = 1.0) -> List[Bucket]:
+    """Greedy bucketing over the arena in ready order (arena must follow that order)."""
+    slots = [arena.slot(i) for i in ready_order]
+    for (s0, e0), (s1, _) in zip(slots, slots[1:]):
+        if s1 != e0:
+            raise ValueError("arena is not laid out in gradient-ready order")
+    buckets: List[Bucket] = []
+    cur: List[int] = []
+    cur_start = None
+    cap = first_bucket_mb * MIB
+    for i, (s, e) in zip(ready_order, slots):
+        if cur_start is None:
+            cur_start = s
+        cur.append(i)
+        if (e - cur_start) * 4 >= cap:
+            buckets.append(Bucket(cur_start, e, cur))
+            cur, cur_start = [], None
+            cap = bucket_mb * MIB
+    if cur:
+        buckets.append(Bucket(cur_start, slots[-1][1], cur))
+    return buckets
+
+
+class BucketedReducer:
+    def __init__(self, arena: FlatArena, ready_order: Sequence[int], bucket_mb: float = 25.0,
+                 first_bucket_mb: float = 1.0, transport: str = "auto", group=None, comm=None):
+        self.arena = arena
+        self.buckets = plan_buckets(arena, ready_order, bucket_mb, first_bucket_mb)
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        dev = arena.grad.device
+        if transport == "auto":
+            transport = "rccl" if dev.type == "cuda" else "torch"
+        self.transport = transport
+        self.param_bucket = [-1] * len(arena.params)
+        for b, bk in enumerate(self.buckets):
+            for i in bk.params:
+                self.param_bucket[i] = b
+        self._native = None
+        if transport == "rccl":
+            from ..ops import _ext
+            C = _ext.require()
+            self.comm = comm or make_rccl_comm(dev, group)
+            self._native = C.BucketReducer(self.comm, arena.grad.data_ptr(),
+                                           [b.start for b in self.buckets], [b.numel for b in self.buckets],
+                                           self.param_bucket, 1)
+        else:
+            self.comm = None
+        self._pending = None
+        self._next = 0
+        self._works = []
+
+    # --------------------------------------------------------------- step API
+    def begin(self):
+        if self._native is not None:
+            self._native.begin()
+            return
+        self._pending = [len(b.params) for b in self.buckets]
+        self._next = 0
+        self._works = []
+
+    def mark_ready(self, params: Sequence[int]):
+        if self._native is not None:
+            from ..ops import _ext
+            self._native.mark_ready(list(params), _ext.stream_ptr(self.arena.grad.device))
+            return
+        for p in params:
+            b = self.param_bucket[p]
+            if b < 0:
+                continue
+            self._pending[b] -= 1
+            if self._pending[b] < 0:
+                raise RuntimeError(f"parameter {p} marked ready twice in one step")
+        while self._next < len(self.buckets) and self._pending[self._next] == 0:
+            self._launch(self._next)
+            self._next += 1
+
+    def _launch(self, b: int):
+        bk = self.buckets[b]
+        view = self.arena.grad[bk.start:bk.end]
+        self._works.append(dist.all_reduce(view, group=self.group, async_op=True))
+
+    def finish(self):
+        if self._native is not None:
+            from ..ops import _ext
+            self._native.finish(_ext.stream_ptr(self.arena.grad.device))
+            return
+        while self._next < len(self.buckets):
+            self._launch(self._next)
+            self._next += 1
+        for w in self._works:
+            w.wait()
+        self._works = []
+
+    def allreduce_scalars(self, t: torch.Tensor):
+        """In-place SUM of a small device vector (loss, non-finite flag) on the compute stream."""
+        if self.world < 2:
+            return t
+        if self._native is not None:
+            from ..ops import _ext
+            self.comm.allreduce(t.data_ptr(), t.numel(), 0, 0, _ext.stream_ptr(t.device))
+        else:
+            dist.all_reduce(t, group=self.group)
+        return t
+
+    def broadcast_arena(self, src: int = 0):
+        """One collective for the whole parameter arena (DDP ctor broadcast, train.py:98-122)."""
+        if self.world < 2:
+            return
+        if self._native is not None:
+            from ..ops import _ext
+            self.comm.broadcast(self.arena.data.data_ptr(), self.arena.numel, 0, src,
+                                _ext.stream_ptr(self.arena.data.device))
+        else:
+            dist.broadcast(self.arena.data, src=src, group=self.group)
+
+    # ------------------------------------------------------- autograd hooks
+    def attach_hooks(self):
+        """Generic autograd path: post-accumulate-grad hooks -> mark_ready (like DDP's reducer hooks)."""
+        handles = []
+        for i, p in enumerate(self.arena.params):
+            def hook(_p, i=i):
+                self.mark_ready([i])
+            handles.append(p.register_post_accumulate_grad_hook(hook))
+        return handles
+
+
+def make_rccl_comm(device, group=None):
+    """Create this process's RCCL communicator; the 128-byte unique id travels
+    through the existing torch process group (one broadcast_object_list)."""
+    from ..ops import _ext
+    C = _ext.require()
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    obj = [C.rccl_unique_id() if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(obj, src=0, group=group)
+    dev = torch.device(device)
+    return C.RcclComm(rank, world, obj[0], dev.index if dev.index is not None else 0)

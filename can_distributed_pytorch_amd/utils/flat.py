@@ -17,13 +17,18 @@ ALIGN = 64
 
 
 class FlatArena:
-    def __init__(self, params: List[torch.nn.Parameter], device, with_grads: bool = True):
+    def __init__(self, params: List[torch.nn.Parameter], device, with_grads: bool = True, order=None):
+        """``order``: parameter indices in the sequence their slots are laid out
+        (gradient-ready order, so reducer buckets are contiguous)."""
         self.params = params
-        self.offsets: List[Tuple[int, int]] = []
+        self.order = list(order) if order is not None else list(range(len(params)))
+        if sorted(self.order) != list(range(len(params))):
+            raise ValueError("order must be a permutation of the parameter indices")
+        self.offsets: List[Tuple[int, int]] = [(0, 0)] * len(params)
         off = 0
-        for p in params:
-            n = p.numel()
-            self.offsets.append((off, n))
+        for i in self.order:
+            n = params[i].numel()
+            self.offsets[i] = (off, n)
             off += (n + ALIGN - 1) // ALIGN * ALIGN
         self.numel = off
         dev = torch.device(device)

@@ -1,0 +1,154 @@
+"""Per-component numerics of the native executor vs plain fp32 PyTorch, and determinism."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+BF16 = torch.bfloat16
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def test_maxpool_fwd_bwd():
+    from can_distributed_pytorch_amd.ops import _ext
+    C = _ext.require()
+    torch.manual_seed(0)
+    n, h, w, c = 2, 12, 20, 64
+    x = torch.relu(torch.randn(n, h, w, c, device="cuda")).to(BF16)
+    y = torch.empty(n, h // 2, w // 2, c, dtype=BF16, device="cuda")
+    C.maxpool_fwd(x.data_ptr(), y.data_ptr(), n, h, w, c, _ext.stream_ptr())
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.max_pool2d(xr, 2, 2)
+    assert torch.equal(y.float(), yr.detach().permute(0, 2, 3, 1))
+    g = torch.randn(n, h // 2, w // 2, c, device="cuda").to(BF16)
+    (gx,) = torch.autograd.grad(yr, xr, g.float().permute(0, 3, 1, 2))
+    ref = gx.permute(0, 2, 3, 1) * (x.float() > 0)
+    dx = torch.empty_like(x)
+    C.maxpool_bwd_relu(x.data_ptr(), g.data_ptr(), dx.data_ptr(), n, h, w, c, _ext.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(dx.float(), ref)
+
+
+def _ctx_ref(fv, w1, w2):
+    """Reference context module (model/CANNet.py:42-87) on NCHW fp32."""
+    h, w = fv.shape[2], fv.shape[3]
+    num = den = None
+    for s in (1, 2, 3, 6):
+        ave = F.conv2d(F.adaptive_avg_pool2d(fv, (s, s)), w1[s])
+        up = F.interpolate(ave, size=(h, w), mode="bilinear", align_corners=True)
+        wt = torch.sigmoid(F.conv2d(up - fv, w2[s]))
+        num = wt * up if num is None else num + wt * up
+        den = wt if den is None else den + wt
+    return torch.cat((fv, num / (den + 1e-12)), 1)
+
+
+@pytest.mark.parametrize("n,h,w", [(2, 12, 16), (1, 13, 22)])
+def test_context_fwd_bwd(n, h, w):
+    from can_distributed_pytorch_amd.models import CANNet
+    from can_distributed_pytorch_amd.ops.executor import CANNetExecutor
+    torch.manual_seed(1)
+    model = CANNet().cuda()
+    for s in (1, 2, 3, 6):
+        torch.nn.init.normal_(getattr(model, f"conv{s}_1").weight, std=0.05)
+        torch.nn.init.normal_(getattr(model, f"conv{s}_2").weight, std=0.05)
+    ex = CANNetExecutor(model)
+    ex.refresh_packs(force=True)
+    fv = torch.relu(torch.randn(n, h, w, 512, device="cuda")).to(BF16)
+    cat, saved = ex._context_fwd(fv, save=True)
+    w1 = {s: getattr(model, f"conv{s}_1").weight.detach() for s in (1, 2, 3, 6)}
+    w2 = {s: getattr(model, f"conv{s}_2").weight.detach().to(BF16).float() for s in (1, 2, 3, 6)}
+    fvr = fv.float().permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    w1r = {s: v.clone().requires_grad_(True) for s, v in w1.items()}
+    w2r = {s: v.clone().requires_grad_(True) for s, v in w2.items()}
+    ref = _ctx_ref(fvr, w1r, w2r)
+    e = _rel(cat.float().permute(0, 3, 1, 2), ref)
+    assert e < 1e-2, f"context fwd rel err {e}"
+    # backward through the executor's context path only
+    dcat = torch.randn(n, h, w, 1024, device="cuda").to(BF16)
+    grads = [torch.zeros_like(p) for p in model.parameters()]
+    gref = torch.autograd.grad(ref, [fvr] + [w1r[s] for s in (1, 2, 3, 6)] + [w2r[s] for s in (1, 2, 3, 6)],
+                               dcat.float().permute(0, 3, 1, 2))
+    dfv = ex._context_bwd(saved, fv, dcat, grads, ex.workspace(n, 8 * h, 8 * w), beta=0.0, scale=1.0,
+                          ready=lambda idx: None)
+    ref_dfv = gref[0].permute(0, 2, 3, 1) * (fv.float() > 0)
+    e = _rel(dfv, ref_dfv)
+    assert e < 3e-2, f"dfv rel err {e}"
+    for k, s in enumerate((1, 2, 3, 6)):
+        e1 = _rel(grads[ex.ctx1_index[s]], gref[1 + k])
+        e2 = _rel(grads[ex.ctx2_index[s]], gref[5 + k])
+        assert e1 < 3e-2 and e2 < 3e-2, (s, e1, e2)
+
+
+def test_head_train():
+    from can_distributed_pytorch_amd.models import CANNet
+    from can_distributed_pytorch_amd.ops.executor import CANNetExecutor
+    torch.manual_seed(2)
+    model = CANNet().cuda()
+    torch.nn.init.normal_(model.output_layer.weight, std=0.1)
+    torch.nn.init.constant_(model.output_layer.bias, 0.3)
+    ex = CANNetExecutor(model)
+    n, h, w = 2, 9, 14
+    b6 = torch.relu(torch.randn(n, h, w, 64, device="cuda")).to(BF16)
+    gt = torch.rand(n, 1, h, w, device="cuda")
+    grads = [torch.zeros_like(p) for p in model.parameters()]
+    loss, et, d_b6 = ex.head_train(b6, gt, grads)
+    x = b6.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = model.output_layer.weight.detach().clone().requires_grad_(True)
+    br = model.output_layer.bias.detach().clone().requires_grad_(True)
+    out = F.conv2d(x, wr, br)
+    lr = ((out - gt) ** 2).sum()
+    gx, gw, gb = torch.autograd.grad(lr, (x, wr, br))
+    assert abs(loss.item() - lr.item()) / lr.item() < 1e-4
+    assert _rel(et, out) < 1e-4
+    assert _rel(d_b6.float(), gx.permute(0, 2, 3, 1) * (b6.float() > 0)) < 1e-2
+    assert _rel(grads[ex.head_w_index], gw) < 1e-4 and _rel(grads[ex.head_b_index], gb) < 1e-4
+
+
+def test_kernels_deterministic():
+    """Same inputs -> bitwise identical outputs (no races in the LDS-DMA pipelines)."""
+    from can_distributed_pytorch_amd.ops import conv as C
+    torch.manual_seed(3)
+    for (n, h, w, ci, co, dil) in [(2, 48, 64, 256, 512, 2), (1, 96, 128, 64, 64, 1), (2, 24, 32, 512, 256, 1)]:
+        x = torch.randn(n, h, w, ci, device="cuda").to(BF16)
+        dy = torch.randn(n, h, w, co, device="cuda").to(BF16)
+        wt = torch.randn(co, ci, 3, 3, device="cuda") * 0.05
+        wf = C.pack_weight_fwd(wt)
+        y1 = C.conv_igemm(x, wf, torch.zeros(co, device="cuda"), ksize=3, dil=dil)
+        y2 = C.conv_igemm(x, wf, torch.zeros(co, device="cuda"), ksize=3, dil=dil)
+        assert torch.equal(y1, y2)
+        d1, d2 = torch.empty_like(wt), torch.empty_like(wt)
+        b1, b2 = torch.empty(co, device="cuda"), torch.empty(co, device="cuda")
+        C.conv_wgrad(dy, x, d1, b1, ksize=3, dil=dil)
+        C.conv_wgrad(dy, x, d2, b2, ksize=3, dil=dil)
+        torch.cuda.synchronize()
+        assert torch.equal(d1, d2) and torch.equal(b1, b2)
+
+
+def test_executor_deterministic():
+    from can_distributed_pytorch_amd.models import CANNet
+    torch.manual_seed(4)
+    m = CANNet().cuda()
+    x = torch.randn(2, 3, 64, 96, device="cuda")
+    gt = torch.rand(2, 1, 8, 12, device="cuda")
+    outs = []
+    for _ in range(2):
+        m.zero_grad(set_to_none=True)
+        loss = torch.nn.MSELoss(reduction="sum")(m(x), gt)
+        loss.backward()
+        outs.append([loss.detach().clone()] + [p.grad.clone() for p in m.parameters()])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+def test_density_gpu_matches_cpu():
+    import numpy as np
+    from can_distributed_pytorch_amd.data.density import density_map_gpu, gaussian_filter_density
+    rng = np.random.default_rng(5)
+    h, w = 96, 128
+    pts = np.stack([rng.random(300) * w, rng.random(300) * h], 1).astype(np.float32)
+    ref = gaussian_filter_density((h, w), pts)
+    got = density_map_gpu(pts, h, w).cpu().numpy()
+    assert np.abs(got - ref).max() < 1e-4
+    assert abs(got.sum() - ref.sum()) < 1e-2
