@@ -309,10 +309,10 @@ __device__ __forceinline__ int swz8b(int row, int c8) {
   else return c8 ^ (((((row >> 1) & 1)) | (((row >> 3) & 1) << 1)) << 2);
 }
 
-template <int WC, int WK, int WM, int NBUF>
+template <int WC, int WK, int WM, int NBUF, int KW>
 __global__ void __launch_bounds__(64 * WC * WK * WM, (WC * WK * WM >= 8) ? 1 : 2) wgrad_glds_kernel(WgradArgs2 a) {
   constexpr int NW = WC * WK * WM;
-  constexpr int TCo = 64 * WC, TK = 64 * WK;
+  constexpr int TCo = 64 * WC, TK = 64 * WK * KW;
   constexpr int BKM = 64 * WM;
   constexpr int RBA = TCo * 2, RBB = TK * 2;
   constexpr int A_BYTES = BKM * RBA, B_BYTES = BKM * RBB;
@@ -347,7 +347,7 @@ __global__ void __launch_bounds__(64 * WC * WK * WM, (WC * WK * WM >= 8) ? 1 : 2
     int lane = tid & 63;
     // small tiles issue many LDS-DMA per stage: keep the compiler from
     // hoisting G address sets out of the loop (they would spill)
-    if constexpr (G > 8) asm volatile("" : "+v"(lane));
+    if constexpr (G > 8 || KW > 1) asm volatile("" : "+v"(lane));
 #pragma unroll
     for (int i = 0; i < G; ++i) {
       const int gi = wave + NW * i;          // wave-uniform
@@ -388,13 +388,13 @@ __global__ void __launch_bounds__(64 * WC * WK * WM, (WC * WK * WM >= 8) ? 1 : 2
     }
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[4][4 * KW];
   f32x4 accb[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     accb[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 4 * KW; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   bf16x8_t ones;
 #pragma unroll
@@ -432,15 +432,15 @@ __global__ void __launch_bounds__(64 * WC * WK * WM, (WC * WK * WM >= 8) ? 1 : 2
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int prow0 = wm * 64 + kk * 32;
-      bf16x8_t af[4], bfr[4];
+      bf16x8_t af[4], bfr[4 * KW];
 #pragma unroll
       for (int j = 0; j < 4; ++j) af[j] = rd(Ab, RBA >= 256, RBA, prow0, wc * 64 + j * 16);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) bfr[i] = rd(Bb, RBB >= 256, RBB, prow0, wk * 64 + i * 16);
+      for (int i = 0; i < 4 * KW; ++i) bfr[i] = rd(Bb, RBB >= 256, RBB, prow0, wk * 64 * KW + i * 16);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4 * KW; ++i)
           acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], bfr[i], acc[j][i], 0, 0, 0);
       if (do_bias && wk == 0) {
 #pragma unroll
@@ -452,12 +452,12 @@ __global__ void __launch_bounds__(64 * WC * WK * WM, (WC * WK * WM >= 8) ? 1 : 2
   // ---- epilogue
   const int fr = lane & 15, fq = lane >> 4;
   float* slab = a.ws + (size_t)slice * a.K * a.Cout;
-  if (WM == 1) {
+  if constexpr (WM == 1) {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int k = k0 + wk * 64 + i * 16 + fr;
+      for (int i = 0; i < 4 * KW; ++i) {
+        const int k = k0 + wk * 64 * KW + i * 16 + fr;
         const int co = co0 + wc * 64 + j * 16 + fq * 4;
         if (k < a.K) *reinterpret_cast<f32x4*>(slab + (size_t)k * a.Cout + co) = acc[j][i];
       }
@@ -469,6 +469,7 @@ __global__ void __launch_bounds__(64 * WC * WK * WM, (WC * WK * WM >= 8) ? 1 : 2
       }
     }
   } else {
+    static_assert(KW == 1, "pixel-split waves use 64x64 wave tiles");
     __syncthreads();
     float* red = reinterpret_cast<float*>(smem);   // [NW][16][64][4] (+ bias [NW][4][64][4])
 #pragma unroll
@@ -515,36 +516,72 @@ __global__ void __launch_bounds__(64 * WC * WK * WM, (WC * WK * WM >= 8) ? 1 : 2
   }
 }
 
-template <int WC, int WK, int WM, int NBUF>
+template <int WC, int WK, int WM, int NBUF, int KW>
 static int launch_wgrad2(const WgradArgs2& a, hipStream_t s) {
   constexpr int NW = WC * WK * WM;
-  constexpr int STAGE = 64 * WM * (64 * WC + 64 * WK) * 2;
+  constexpr int STAGE = 64 * WM * (64 * WC + 64 * WK * KW) * 2;
   size_t lds = (size_t)NBUF * STAGE;
   if (WM > 1) lds = std::max(lds, (size_t)(NW * 16 * 64 * 4 + NW * 4 * 64 * 4) * 4);
-  auto kfn = wgrad_glds_kernel<WC, WK, WM, NBUF>;
+  auto kfn = wgrad_glds_kernel<WC, WK, WM, NBUF, KW>;
   static bool attr = false;
   if (!attr) {
     CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
-  const int ntile = (a.Cout / (64 * WC)) * ((a.K + 64 * WK - 1) / (64 * WK));
+  const int ntile = (a.Cout / (64 * WC)) * ((a.K + 64 * WK * KW - 1) / (64 * WK * KW));
   hipLaunchKernelGGL(kfn, dim3(ntile * a.S), dim3(64 * NW), lds, s, a);
   return (int)hipGetLastError();
 }
 
-// Sum S slabs [S][Ktot][Cout] in fixed order and write dW in the PyTorch
-// layout [Cout][Cin][kh][kw] (first layer: Cin = 3 real channels of the
-// k = tap*4 + c packing).  beta = 0 overwrites, 1 accumulates.
+// Sum S slabs [S][K][Cout] in a fixed order and write dW in the PyTorch layout
+// [Cout][Cin][kh][kw] (first layer: Cin = 3 real channels of the k = tap*4 + c
+// packing).  beta = 0 overwrites, 1 accumulates.  Block = 64 consecutive
+// elements x 4 slice groups (each thread sums a strided quarter of the slices
+// with 4 independent accumulators), combined in LDS in a fixed order:
+// deterministic, and enough loads in flight for S in the hundreds.
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ ws, const float* __restrict__ wsb,
                                                            float* __restrict__ dw, float* __restrict__ db, int S,
                                                            int Ktot, int Cout, int Cin, int taps, int first,
                                                            float beta, float scale) {
-  const int idx = blockIdx.x * 256 + threadIdx.x;   // over Ktot*Cout, co fastest
+  __shared__ float part[4][64];
+  const int e = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const size_t plane = (size_t)Ktot * Cout;
-  if (idx < plane) {
-    float s = 0.f;
-    for (int sl = 0; sl < S; ++sl) s += ws[sl * plane + idx];
-    s *= scale;
+  const size_t idx = (size_t)blockIdx.x * 64 + e;
+  const bool is_bias = blockIdx.x == gridDim.x - 1;      // last block: bias
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (!is_bias) {
+    if (idx < plane) {
+      int sl = grp;
+      for (; sl + 12 < S; sl += 16) {
+        s0 += ws[(size_t)sl * plane + idx];
+        s1 += ws[(size_t)(sl + 4) * plane + idx];
+        s2 += ws[(size_t)(sl + 8) * plane + idx];
+        s3 += ws[(size_t)(sl + 12) * plane + idx];
+      }
+      for (; sl < S; sl += 4) s0 += ws[(size_t)sl * plane + idx];
+    }
+  } else if (db != nullptr) {
+    for (int c0 = 0; c0 < Cout; c0 += 64) {
+      const int c = c0 + e;
+      float t = 0.f;
+      if (c < Cout)
+        for (int sl = grp; sl < S; sl += 4) t += wsb[(size_t)sl * Cout + c];
+      part[grp][e] = t;
+      __syncthreads();
+      if (grp == 0 && c < Cout) {
+        const float v = (part[0][e] + part[1][e] + part[2][e] + part[3][e]) * scale;
+        db[c] = (beta != 0.f) ? db[c] * beta + v : v;
+      }
+      __syncthreads();
+    }
+    return;
+  } else {
+    return;
+  }
+  part[grp][e] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (grp == 0 && idx < plane) {
+    const float v = (part[0][e] + part[1][e] + part[2][e] + part[3][e]) * scale;
     const int co = idx % Cout, k = idx / Cout;
     int ci, tap;
     bool valid = true;
@@ -553,14 +590,8 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
     if (valid) {
       const int cin_t = first ? 3 : Cin;
       float* o = dw + ((size_t)co * cin_t + ci) * taps + tap;
-      *o = (beta != 0.f) ? (*o * beta + s) : s;
+      *o = (beta != 0.f) ? (*o * beta + v) : v;
     }
-  }
-  if (db != nullptr && idx < Cout) {
-    float s = 0.f;
-    for (int sl = 0; sl < S; ++sl) s += wsb[(size_t)sl * Cout + idx];
-    s *= scale;
-    db[idx] = (beta != 0.f) ? (db[idx] * beta + s) : s;
   }
 }
 
@@ -594,6 +625,8 @@ static void wgrad_tile(int cfg, int* TCo, int* TK, int* BKM) {
     case 2: *TCo = 256; *TK = 128; *BKM = 64; break;
     case 3: *TCo = 64; *TK = 128; *BKM = 128; break;
     case 4: *TCo = 64; *TK = 64; *BKM = 128; break;
+    case 5: *TCo = 256; *TK = 256; *BKM = 64; break;
+    case 6: *TCo = 128; *TK = 256; *BKM = 64; break;
     default: *TCo = 64; *TK = 64; *BKM = 128; break;
   }
 }
@@ -603,7 +636,9 @@ extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, in
   const int K = first ? 64 : ksize * ksize * Cin;
   int cfg;
   if (first) cfg = 0;
+  else if (Cout % 256 == 0 && K >= 2048) cfg = 5;
   else if (Cout % 256 == 0 && K >= 1024) cfg = 2;
+  else if (Cout % 128 == 0 && K >= 2048) cfg = 6;
   else if (Cout % 128 == 0) cfg = 1;
   else if (K >= 128) cfg = 3;
   else cfg = 4;
@@ -654,16 +689,18 @@ extern "C" int can_conv_wgrad(const void* dy, const void* x, float* ws, float* w
     a.S = S; a.mslice = mslice;
     a.fdW = make_fastdiv((uint32_t)W); a.fdH = make_fastdiv((uint32_t)H); a.fdC = make_fastdiv((uint32_t)Cin);
     switch (cfg) {
-      case 1: if (Cout % 128) return -4; rc = launch_wgrad2<2, 2, 1, 4>(a, s); break;
-      case 2: if (Cout % 256) return -4; rc = launch_wgrad2<4, 2, 1, 3>(a, s); break;
-      case 3: rc = launch_wgrad2<1, 2, 2, 3>(a, s); break;
-      case 4: rc = launch_wgrad2<1, 1, 2, 4>(a, s); break;
+      case 1: if (Cout % 128) return -4; rc = launch_wgrad2<2, 2, 1, 4, 1>(a, s); break;
+      case 2: if (Cout % 256) return -4; rc = launch_wgrad2<4, 2, 1, 3, 1>(a, s); break;
+      case 3: rc = launch_wgrad2<1, 2, 2, 3, 1>(a, s); break;
+      case 4: rc = launch_wgrad2<1, 1, 2, 4, 1>(a, s); break;
+      case 5: if (Cout % 256) return -4; rc = launch_wgrad2<4, 2, 1, 2, 2>(a, s); break;
+      case 6: if (Cout % 128) return -4; rc = launch_wgrad2<2, 2, 1, 3, 2>(a, s); break;
       default: return -5;
     }
   }
   if (rc) return rc;
   const int plane = K * Cout;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((plane + 255) / 256), dim3(256), 0, s, ws, wsb_used, dw, db, S, K,
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((plane + 63) / 64 + 1), dim3(256), 0, s, ws, wsb_used, dw, db, S, K,
                      Cout, first ? 4 : Cin, ksize * ksize, first, beta, scale);
   return (int)hipGetLastError();
 }
