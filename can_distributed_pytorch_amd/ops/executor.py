@@ -107,7 +107,8 @@ class CANNetExecutor:
         for s in self.front + self.back:
             w = s.module.weight
             if s.first:
-                fwd = torch.empty(s.cout, 64, dtype=BF16, device=device)
+                # k = tap*4 + c: the pack kernel writes only c < 3, tap < 9 -> pad must be zero
+                fwd = torch.zeros(s.cout, 64, dtype=BF16, device=device)
                 dgr = None
             else:
                 fwd = torch.empty(s.cout, s.ksize * s.ksize * s.cin, dtype=BF16, device=device)

@@ -1,0 +1,3 @@
+#!/bin/bash
+cd "$GRAFT_REPO_ROOT" || exit 2
+scripts/gpu/run_step.sh debug_eval 300 python scripts/debug_eval.py || exit $?

@@ -152,3 +152,27 @@ def test_density_gpu_matches_cpu():
     got = density_map_gpu(pts, h, w).cpu().numpy()
     assert np.abs(got - ref).max() < 1e-4
     assert abs(got.sum() - ref.sum()) < 1e-2
+
+
+def test_no_uninitialized_reads_poisoned_allocator():
+    """Regression: fill the caching allocator with NaN bit patterns before every
+    buffer the executor allocates; outputs must not change (a NaN read from an
+    unwritten pad once got silently zeroed by fmaxf in a ReLU epilogue)."""
+    from can_distributed_pytorch_amd.models import CANNet
+    torch.manual_seed(6)
+    x = torch.randn(2, 3, 64, 96, device="cuda")
+    outs = []
+    for bits in (0, 0x7FC07FC0):
+        m = CANNet().cuda()
+        torch.manual_seed(7)
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.Conv2d):
+                torch.nn.init.normal_(mod.weight, std=0.05)
+        t = torch.empty(256 * 1024 * 1024 // 4, dtype=torch.int32, device="cuda")
+        t.fill_(bits)
+        del t
+        with torch.no_grad():
+            outs.append(m(x))
+        torch.cuda.synchronize()
+    assert not torch.isnan(outs[1]).any()
+    assert torch.equal(outs[0], outs[1])

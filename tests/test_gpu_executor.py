@@ -49,7 +49,7 @@ def test_executor_forward(n, h, w):
         _, ya = _autocast(ref, x)
     assert yn.shape == yr.shape == (n, 1, h // 8, w // 8)
     en, ea = _rel(yn, yr), _rel(ya, yr)
-    assert en < max(1.5 * ea, 0.02), (en, ea)
+    assert en < max(1.5 * ea, 0.01), (en, ea)
 
 
 def test_executor_backward_grads():
