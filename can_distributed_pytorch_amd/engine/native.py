@@ -34,7 +34,8 @@ from ..utils.flat import FlatArena
 
 class NativeStepper:
     def __init__(self, device, dtype="bf16", world=1, lr=1e-7, momentum=0.95, batch=8, height=768, width=1024,
-                 graph=True, model: Optional[CANNet] = None, reducer=None, bucket_mb: float = 25.0):
+                 graph=True, model: Optional[CANNet] = None, reducer=None, bucket_mb: float = 25.0,
+                 reducer_transport: Optional[str] = None):
         if dtype != "bf16":
             raise ValueError("the native step computes in bf16 (fp32 master weights); use --impl torch for fp32")
         self.C = _ext.require()
@@ -53,9 +54,10 @@ class NativeStepper:
         self.grads = self.arena.grad_views()
         self.flags = torch.zeros(4, dtype=torch.float32, device=self.device)   # [nonfinite, loss, ...]
         self.reducer = reducer
-        if self.reducer is None and world > 1:
+        if self.reducer is None and (world > 1 or reducer_transport is not None):
             from ..parallel.reducer import BucketedReducer
-            self.reducer = BucketedReducer(self.arena, self.ex.grad_ready_order(), bucket_mb=bucket_mb)
+            self.reducer = BucketedReducer(self.arena, self.ex.grad_ready_order(), bucket_mb=bucket_mb,
+                                           transport=reducer_transport or "auto")
         if world > 1:
             self._broadcast_params()
         self.use_graph = graph

@@ -124,3 +124,23 @@ def test_loss_decreases_native():
     st = NativeStepper("cuda", lr=1e-6, graph=False, model=m)
     losses = [float(st.step(img, gt)) for _ in range(8)]
     assert losses[-1] < losses[0], losses
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_native_stepper_with_rccl_reducer_world1(graph):
+    """The C++ RCCL bucketed reducer (1-rank communicator) inside the native step, eager and hipGraph-captured:
+    results must equal the reducer-free step (a 1-rank all-reduce is the identity)."""
+    from can_distributed_pytorch_amd.engine.native import NativeStepper
+    _, nat_a = _models(4)
+    nat_b = copy.deepcopy(nat_a)
+    x = torch.randn(1, 3, 64, 64, device="cuda")
+    gt = torch.rand(1, 1, 8, 8, device="cuda")
+    a = NativeStepper("cuda", lr=1e-7, graph=graph, model=nat_a)
+    b = NativeStepper("cuda", lr=1e-7, graph=graph, model=nat_b, reducer_transport="rccl", bucket_mb=4.0)
+    assert b.reducer is not None and b.reducer.transport == "rccl" and len(b.reducer.buckets) >= 4
+    for _ in range(3):
+        a.step(x, gt)
+        b.step(x, gt)
+    torch.cuda.synchronize()
+    for pa, pb in zip(nat_a.parameters(), nat_b.parameters()):
+        assert torch.equal(pa, pb)

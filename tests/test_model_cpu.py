@@ -1,0 +1,141 @@
+"""CPU tier: model API parity with the reference, checkpoints, flat arena, entry points."""
+import collections
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_state_dict_parity():
+    from can_distributed_pytorch_amd.models import CANNet, reference_state_dict_keys
+    m = CANNet()
+    sd = m.state_dict()
+    assert list(sd.keys()) == reference_state_dict_keys()
+    assert sum(p.numel() for p in m.parameters()) == 20_719_937
+    assert len(sd) == 42
+    assert sd["backend.0.weight"].shape == (512, 1024, 3, 3)
+    assert sd["output_layer.weight"].shape == (1, 64, 1, 1)
+    assert sd["conv6_2.weight"].shape == (512, 512, 1, 1)
+    dil = [m for m in m._modules["backend"] if isinstance(m, torch.nn.Conv2d)]
+    assert all(c.dilation == (2, 2) and c.padding == (2, 2) for c in dil)
+
+
+def test_init_matches_reference_distribution():
+    from can_distributed_pytorch_amd.models import CANNet
+    torch.manual_seed(0)
+    m = CANNet()
+    w = m.backend[0].weight
+    assert abs(w.std().item() - 0.01) < 5e-4 and abs(w.mean().item()) < 1e-4
+    assert torch.all(m.backend[0].bias == 0)
+
+
+def test_baseline_config1_cpu_forward_mse():
+    """BASELINE config #1: CANNet forward + MSE on one 256x256 image, CPU, world_size=1."""
+    from can_distributed_pytorch_amd.models import CANNet
+    torch.manual_seed(0)
+    m = CANNet()
+    x = torch.randn(1, 3, 256, 256)
+    y = m(x)
+    assert y.shape == (1, 1, 32, 32)
+    loss = torch.nn.MSELoss(reduction="sum")(y, torch.rand(1, 1, 32, 32))
+    loss.backward()
+    assert torch.isfinite(loss)
+    assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in m.parameters())
+
+
+def test_checkpoint_roundtrip_both_layouts(tmp_path):
+    from can_distributed_pytorch_amd.models import CANNet
+    from can_distributed_pytorch_amd.utils.checkpoint import save_checkpoint, load_checkpoint
+    torch.manual_seed(1)
+    a = CANNet()
+    p = tmp_path / "plain.pth"
+    save_checkpoint(a, str(p))
+    b = CANNet()
+    load_checkpoint(b, str(p))
+    assert all(torch.equal(x, y) for x, y in zip(a.state_dict().values(), b.state_dict().values()))
+    # the reference's own DDP checkpoint layout (train.py:161): module.-prefixed keys
+    ddp = collections.OrderedDict(("module." + k, v) for k, v in a.state_dict().items())
+    q = tmp_path / "ddp.pth"
+    torch.save(ddp, q)
+    c = CANNet()
+    res = load_checkpoint(c, str(q), strict=True)
+    assert not res.missing_keys and not res.unexpected_keys
+    assert torch.equal(c.conv3_2.weight, a.conv3_2.weight)
+    c2 = CANNet()
+    c2.load_state_dict(ddp)            # model.load_state_dict accepts it directly too
+    assert torch.equal(c2.frontend[0].weight, a.frontend[0].weight)
+
+
+def test_vgg16_positional_transfer(tmp_path):
+    from can_distributed_pytorch_amd.models import CANNet
+    feats = collections.OrderedDict()
+    cfg = [(3, 64), (64, 64), "M", (64, 128), (128, 128), "M", (128, 256), (256, 256), (256, 256), "M",
+           (256, 512), (512, 512), (512, 512), "M", (512, 512), (512, 512), (512, 512)]
+    i = 0
+    for c in cfg:
+        if c == "M":
+            i += 1
+            continue
+        feats[f"features.{i}.weight"] = torch.full((c[1], c[0], 3, 3), float(i))
+        feats[f"features.{i}.bias"] = torch.full((c[1],), float(i))
+        i += 2
+    path = tmp_path / "vgg16.pth"
+    torch.save(feats, path)
+    m = CANNet(vgg16_path=str(path))
+    # features.{0,2,5,7,10,12,14,17,19,21} -> frontend.{same}
+    for idx in (0, 2, 5, 7, 10, 12, 14, 17, 19, 21):
+        assert torch.all(m.frontend[idx].weight == float(idx))
+
+
+def test_flat_arena_views():
+    from can_distributed_pytorch_amd.models import CANNet
+    from can_distributed_pytorch_amd.utils.flat import FlatArena
+    m = CANNet()
+    params = list(m.parameters())
+    before = [p.detach().clone() for p in params]
+    order = list(reversed(range(len(params))))
+    ar = FlatArena(params, "cpu", order=order)
+    for p, b in zip(params, before):
+        assert torch.equal(p, b)
+        assert p.data.data_ptr() >= ar.data.data_ptr()
+    ar.data.add_(1.0)
+    assert torch.equal(params[0], before[0] + 1)
+    assert ar.slot(order[0])[0] == 0
+    assert ar.numel % 64 == 0
+
+
+def test_compat_imports():
+    sys.path.insert(0, ROOT)
+    from model import CANNet, CrowdDataset  # noqa: F401
+    from model.CANNet import CANNet as C2  # noqa: F401
+    from utils.distributed_utils import reduce_value, init_distributed_mode, is_main_process  # noqa: F401
+    from utils.train_eval_utils import train_one_epoch, evaluate  # noqa: F401
+
+
+def test_bench_json_contract_cpu_stub():
+    """bench.py must parse its flags (full run needs a GPU)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--help"], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0 and "--gpus" in r.stdout and "--steps" in r.stdout and "--warmup" in r.stdout
+
+
+@pytest.mark.slow
+def test_train_py_two_rank_gloo(tmp_path):
+    """train.py end to end on a 2-rank gloo fake cluster (CPU, stock impl), then test.py on its checkpoint."""
+    env = dict(os.environ, OMP_NUM_THREADS="2", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=29631", os.path.join(ROOT, "train.py"),
+           "--device", "cpu", "--synthetic", "32x48", "--synthetic-n", "8", "--epochs", "1", "--batch-size", "2",
+           "--num-workers", "0", "--wandb", "false", "--show", "false", "--checkpoint-dir", str(tmp_path),
+           "--log-jsonl", str(tmp_path / "m.jsonl")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert (tmp_path / "epoch_0.pth").exists() and (tmp_path / "last_state.pth").exists()
+    r2 = subprocess.run([sys.executable, os.path.join(ROOT, "test.py"), "--synthetic", "32x48", "--checkpoint",
+                         str(tmp_path / "epoch_0.pth"), "--device", "cpu"], capture_output=True, text=True,
+                        timeout=300)
+    assert r2.returncode == 0 and "mae:" in r2.stdout, r2.stderr[-2000:]
