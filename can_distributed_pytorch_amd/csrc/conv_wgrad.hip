@@ -29,6 +29,7 @@
 //            of every stage; the 4 partial tiles are summed through LDS.
 #include "common.h"
 #include "fastdiv.h"
+#include <stdlib.h>
 
 namespace can {
 
@@ -309,11 +310,11 @@ __device__ __forceinline__ int swz8b(int row, int c8) {
   else return c8 ^ (((((row >> 1) & 1)) | (((row >> 3) & 1) << 1)) << 2);
 }
 
-template <int WC, int WK, int WM, int NBUF, int KW>
+template <int WC, int WK, int WM, int NBUF, int KW, int KK>
 __global__ void __launch_bounds__(64 * WC * WK * WM, (WC * WK * WM >= 8) ? 1 : 2) wgrad_glds_kernel(WgradArgs2 a) {
   constexpr int NW = WC * WK * WM;
   constexpr int TCo = 64 * WC, TK = 64 * WK * KW;
-  constexpr int BKM = 64 * WM;
+  constexpr int BKM = 32 * KK * WM;              // pixels per stage (KK 32-deep MFMA steps per wave)
   constexpr int RBA = TCo * 2, RBB = TK * 2;
   constexpr int A_BYTES = BKM * RBA, B_BYTES = BKM * RBB;
   constexpr int STAGE = A_BYTES + B_BYTES;
@@ -430,8 +431,8 @@ __global__ void __launch_bounds__(64 * WC * WK * WM, (WC * WK * WM >= 8) ? 1 : 2
     const unsigned char* Ab = smem + (st % NBUF) * STAGE;
     const unsigned char* Bb = Ab + A_BYTES;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int prow0 = wm * 64 + kk * 32;
+    for (int kk = 0; kk < KK; ++kk) {
+      const int prow0 = wm * 32 * KK + kk * 32;
       bf16x8_t af[4], bfr[4 * KW];
 #pragma unroll
       for (int j = 0; j < 4; ++j) af[j] = rd(Ab, RBA >= 256, RBA, prow0, wc * 64 + j * 16);
@@ -516,13 +517,13 @@ __global__ void __launch_bounds__(64 * WC * WK * WM, (WC * WK * WM >= 8) ? 1 : 2
   }
 }
 
-template <int WC, int WK, int WM, int NBUF, int KW>
+template <int WC, int WK, int WM, int NBUF, int KW, int KK>
 static int launch_wgrad2(const WgradArgs2& a, hipStream_t s) {
   constexpr int NW = WC * WK * WM;
-  constexpr int STAGE = 64 * WM * (64 * WC + 64 * WK * KW) * 2;
+  constexpr int STAGE = 32 * KK * WM * (64 * WC + 64 * WK * KW) * 2;
   size_t lds = (size_t)NBUF * STAGE;
   if (WM > 1) lds = std::max(lds, (size_t)(NW * 16 * 64 * 4 + NW * 4 * 64 * 4) * 4);
-  auto kfn = wgrad_glds_kernel<WC, WK, WM, NBUF, KW>;
+  auto kfn = wgrad_glds_kernel<WC, WK, WM, NBUF, KW, KK>;
   static bool attr = false;
   if (!attr) {
     CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -625,8 +626,9 @@ static void wgrad_tile(int cfg, int* TCo, int* TK, int* BKM) {
     case 2: *TCo = 256; *TK = 128; *BKM = 64; break;
     case 3: *TCo = 64; *TK = 128; *BKM = 128; break;
     case 4: *TCo = 64; *TK = 64; *BKM = 128; break;
-    case 5: *TCo = 256; *TK = 256; *BKM = 64; break;
+    case 5: *TCo = 256; *TK = 256; *BKM = 32; break;
     case 6: *TCo = 128; *TK = 256; *BKM = 64; break;
+    case 7: *TCo = 256; *TK = 256; *BKM = 64; break;
     default: *TCo = 64; *TK = 64; *BKM = 128; break;
   }
 }
@@ -634,6 +636,7 @@ static void wgrad_tile(int cfg, int* TCo, int* TK, int* BKM) {
 extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, int target_blocks, int* S_out,
                               int* mslice_out, int* cfg_out) {
   const int K = first ? 64 : ksize * ksize * Cin;
+  const char* force = getenv("CANNET_WGRAD_CFG");
   int cfg;
   if (first) cfg = 0;
   else if (Cout % 256 == 0 && K >= 2048) cfg = 5;
@@ -642,10 +645,13 @@ extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, in
   else if (Cout % 128 == 0) cfg = 1;
   else if (K >= 128) cfg = 3;
   else cfg = 4;
+  if (force && !first) cfg = atoi(force);
   int TCo, TK, BKM;
   wgrad_tile(cfg, &TCo, &TK, &BKM);
   const int ntile = (Cout / TCo) * ((K + TK - 1) / TK);
-  int S = (target_blocks + ntile - 1) / ntile;
+  // whole rounds of co-resident blocks (no half-empty last round)
+  int S = target_blocks / ntile;
+  if (S < 1) S = 1;
   const int max_s = (M + BKM - 1) / BKM;
   if (S > max_s) S = max_s;
   if (S < 1) S = 1;
@@ -689,12 +695,13 @@ extern "C" int can_conv_wgrad(const void* dy, const void* x, float* ws, float* w
     a.S = S; a.mslice = mslice;
     a.fdW = make_fastdiv((uint32_t)W); a.fdH = make_fastdiv((uint32_t)H); a.fdC = make_fastdiv((uint32_t)Cin);
     switch (cfg) {
-      case 1: if (Cout % 128) return -4; rc = launch_wgrad2<2, 2, 1, 4, 1>(a, s); break;
-      case 2: if (Cout % 256) return -4; rc = launch_wgrad2<4, 2, 1, 3, 1>(a, s); break;
-      case 3: rc = launch_wgrad2<1, 2, 2, 3, 1>(a, s); break;
-      case 4: rc = launch_wgrad2<1, 1, 2, 4, 1>(a, s); break;
-      case 5: if (Cout % 256) return -4; rc = launch_wgrad2<4, 2, 1, 2, 2>(a, s); break;
-      case 6: if (Cout % 128) return -4; rc = launch_wgrad2<2, 2, 1, 3, 2>(a, s); break;
+      case 1: if (Cout % 128) return -4; rc = launch_wgrad2<2, 2, 1, 4, 1, 2>(a, s); break;
+      case 2: if (Cout % 256) return -4; rc = launch_wgrad2<4, 2, 1, 3, 1, 2>(a, s); break;
+      case 3: rc = launch_wgrad2<1, 2, 2, 3, 1, 2>(a, s); break;
+      case 4: rc = launch_wgrad2<1, 1, 2, 4, 1, 2>(a, s); break;
+      case 5: if (Cout % 256) return -4; rc = launch_wgrad2<4, 2, 1, 4, 2, 1>(a, s); break;
+      case 6: if (Cout % 128) return -4; rc = launch_wgrad2<2, 2, 1, 3, 2, 2>(a, s); break;
+      case 7: if (Cout % 256) return -4; rc = launch_wgrad2<4, 2, 1, 2, 2, 2>(a, s); break;
       default: return -5;
     }
   }
