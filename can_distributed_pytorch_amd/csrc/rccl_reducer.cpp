@@ -211,8 +211,10 @@ void register_rccl(py::module_& m) {
     return v;
   });
   py::class_<RcclComm>(m, "RcclComm")
-      .def(py::init([](int rank, int world, py::bytes uid, int device) {
-             return new RcclComm(rank, world, std::string(uid), device);
+      // uid arrives as std::string: converted from bytes BEFORE the GIL is
+      // released (ncclCommInitRank blocks until every rank has joined)
+      .def(py::init([](int rank, int world, std::string uid, int device) {
+             return new RcclComm(rank, world, uid, device);
            }),
            py::call_guard<py::gil_scoped_release>())
       .def("allreduce", &RcclComm::allreduce)
