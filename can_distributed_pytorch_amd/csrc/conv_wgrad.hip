@@ -639,7 +639,7 @@ extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, in
   const char* force = getenv("CANNET_WGRAD_CFG");
   int cfg;
   if (first) cfg = 0;
-  else if (Cout % 256 == 0 && K >= 2048) cfg = 5;
+  else if (Cout % 256 == 0 && K >= 2048) cfg = 7;
   else if (Cout % 256 == 0 && K >= 1024) cfg = 2;
   else if (Cout % 128 == 0 && K >= 2048) cfg = 6;
   else if (Cout % 128 == 0) cfg = 1;
