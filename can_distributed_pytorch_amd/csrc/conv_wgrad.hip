@@ -30,6 +30,7 @@
 #include "common.h"
 #include "fastdiv.h"
 #include <stdlib.h>
+#include <type_traits>
 
 namespace can {
 
@@ -534,6 +535,176 @@ static int launch_wgrad2(const WgradArgs2& a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// ===========================================================================
+// Halo-tiled weight gradient for 3x3 / dilation-1 layers with Cin % 64 == 0 and
+// Cout in {64, 128} (the high-resolution VGG layers conv1_2, conv2_1, conv2_2).
+//
+// The generic kernel re-streams dY once per k-tile and X once per co-tile
+// from HBM (dY/X of conv1_2 are 0.8 GB each at batch 8) and its 64-wide tiles
+// are L2-bound.  Here one block stages an output tile of TH x 64 pixels of dY
+// plus the (TH+2) x 66 input halo of one 64-channel slice of X ONCE, and its 9
+// waves - one per tap - read their shifted windows of the same halo with
+// transposed LDS reads: every byte is fetched once per block-stage and feeds
+// 9 taps.  Out tile per block = Cout x (9 taps x 64 ci); partial slabs and the
+// deterministic reduction are shared with the generic kernel.
+// ===========================================================================
+struct HaloArgs {
+  const bf16_t* dy;
+  const bf16_t* x;
+  const bf16_t* zero;
+  float* ws;
+  float* wsb;
+  int N, H, W, Cin, Cout, K, S;
+  int tiles_y, tiles_x, ntiles, tiles_per_slice;
+};
+
+template <int CO, int TH>
+__global__ void __launch_bounds__(576, 1) wgrad_halo_kernel(HaloArgs a) {
+  constexpr int TW = 64;
+  constexpr int HW_ = TW + 2;                       // halo width
+  constexpr int HH = TH + 2;                        // halo height
+  constexpr int NPIX = TH * TW;
+  constexpr int RBD = CO * 2;                       // dY row bytes
+  constexpr int DY_BYTES = NPIX * RBD;
+  constexpr int X_BYTES = ((HH * HW_ * 128 + 1023) / 1024) * 1024;
+  constexpr int STAGE = DY_BYTES + X_BYTES;
+  constexpr int NID = DY_BYTES / 1024;              // LDS-DMA instructions per stage
+  constexpr int NIX = X_BYTES / 1024;
+  constexpr int NT = CO / 16;                       // co tiles of 16
+
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);     // = tap
+  const int kh = wave / 3, kw = wave % 3;
+  const int nci = a.Cin >> 6, nco = a.Cout / CO;
+  const int ci_t = blockIdx.x % nci;
+  const int co0 = ((blockIdx.x / nci) % nco) * CO;
+  const int slice = blockIdx.x / (nci * nco);
+  const int ci0 = ci_t * 64;
+  const int t_beg = slice * a.tiles_per_slice;
+  const int t_end = min(a.ntiles, t_beg + a.tiles_per_slice);
+  const int nstage = max(0, t_end - t_beg);
+  const bool do_bias = (a.wsb != nullptr) && ci_t == 0 && wave == 4;
+
+  auto issue = [&](int st, int buf) {
+    const int t = t_beg + st;
+    const int n = t / (a.tiles_y * a.tiles_x);
+    const int rem = t - n * a.tiles_y * a.tiles_x;
+    const int y0 = (rem / a.tiles_x) * TH, x0 = (rem % a.tiles_x) * TW;
+    unsigned char* sbase = smem + buf * STAGE;
+    for (int i = wave; i < NID + NIX; i += 9) {
+      const void* src = a.zero;
+      unsigned char* dst;
+      if (i < NID) {
+        const int byte = i * 1024 + lane * 16;
+        const int p = byte / RBD;
+        const int lc16 = swz8b<RBD>(p, ((byte % RBD) / 16) * 2) >> 1;
+        const int yy = y0 + p / TW, xx = x0 + p % TW;
+        if (yy < a.H && xx < a.W) src = a.dy + ((size_t)(n * a.H + yy) * a.W + xx) * a.Cout + co0 + lc16 * 8;
+        dst = sbase + i * 1024;
+      } else {
+        const int byte = (i - NID) * 1024 + lane * 16;
+        const int q = byte / 128;
+        const int lc16 = swz8b<128>(q, ((byte % 128) / 16) * 2) >> 1;
+        const int yy = y0 - 1 + q / HW_, xx = x0 - 1 + q % HW_;
+        if (q < HH * HW_ && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W)
+          src = a.x + ((size_t)(n * a.H + yy) * a.W + xx) * a.Cin + ci0 + lc16 * 8;
+        dst = sbase + DY_BYTES + (i - NID) * 1024;
+      }
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[NT][4];
+  f32x4 accb[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    accb[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  bf16x8_t ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  // transposed read of 8 consecutive rows r0.. (pixels) at column col0 of an LDS image with RB-byte rows
+  auto rd = [&](const unsigned char* base, auto rbc, int prow0, int col0) -> bf16x8_t {
+    constexpr int RB = decltype(rbc)::value;
+    const int r0 = prow0 + 8 * g + q;
+    const int c8 = (col0 >> 2) + p;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + r0 * RB + swz8b<RB>(r0, c8) * 8));
+    const s16x4 hi =
+        __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + (r0 + 4) * RB + swz8b<RB>(r0 + 4, c8) * 8));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8_t, v);
+  };
+  using RBdy = std::integral_constant<int, RBD>;
+  using RBx = std::integral_constant<int, 128>;
+
+  if (nstage > 0) issue(0, 0);
+  for (int st = 0; st < nstage; ++st) {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (st + 1 < nstage) issue(st + 1, (st + 1) & 1);
+    const unsigned char* Db = smem + (st & 1) * STAGE;
+    const unsigned char* Xb = Db + DY_BYTES;
+#pragma unroll
+    for (int r = 0; r < TH; ++r) {
+#pragma unroll
+      for (int gg = 0; gg < TW / 32; ++gg) {
+        const int prow_d = r * TW + gg * 32;
+        const int prow_x = (r + kh) * HW_ + gg * 32 + kw;
+        bf16x8_t af[NT], bfr[4];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) af[j] = rd(Db, RBdy{}, prow_d, j * 16);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bfr[i] = rd(Xb, RBx{}, prow_x, i * 16);
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], bfr[i], acc[j][i], 0, 0, 0);
+        if (do_bias) {
+#pragma unroll
+          for (int j = 0; j < NT; ++j) accb[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], ones, accb[j], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // epilogue: slab[slice][k = tap*Cin + ci][co]
+  const int fr = lane & 15, fq = lane >> 4;
+  float* slab = a.ws + (size_t)slice * a.K * a.Cout;
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = wave * a.Cin + ci0 + i * 16 + fr;
+      const int co = co0 + j * 16 + fq * 4;
+      *reinterpret_cast<f32x4*>(slab + (size_t)k * a.Cout + co) = acc[j][i];
+    }
+  if (do_bias && fr == 0) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+      *reinterpret_cast<f32x4*>(a.wsb + (size_t)slice * a.Cout + co0 + j * 16 + fq * 4) = accb[j];
+  }
+}
+
+template <int CO, int TH>
+static int launch_halo(HaloArgs& a, hipStream_t s) {
+  constexpr int TW = 64;
+  constexpr int DY_BYTES = TH * TW * CO * 2;
+  constexpr int X_BYTES = (((TH + 2) * (TW + 2) * 128 + 1023) / 1024) * 1024;
+  const size_t lds = 2 * (size_t)(DY_BYTES + X_BYTES);
+  auto kfn = wgrad_halo_kernel<CO, TH>;
+  static bool attr = false;
+  if (!attr) {
+    CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  hipLaunchKernelGGL(kfn, dim3((a.Cin / 64) * (a.Cout / CO) * a.S), dim3(576), lds, s, a);
+  return (int)hipGetLastError();
+}
+
 // Sum S slabs [S][K][Cout] in a fixed order and write dW in the PyTorch layout
 // [Cout][Cin][kh][kw] (first layer: Cin = 3 real channels of the k = tap*4 + c
 // packing).  beta = 0 overwrites, 1 accumulates.  Block = 64 consecutive
@@ -629,6 +800,7 @@ static void wgrad_tile(int cfg, int* TCo, int* TK, int* BKM) {
     case 5: *TCo = 256; *TK = 256; *BKM = 32; break;
     case 6: *TCo = 128; *TK = 256; *BKM = 64; break;
     case 7: *TCo = 256; *TK = 256; *BKM = 64; break;
+    case 8: *TCo = 0; *TK = 0; *BKM = 128; break;   // halo kernel: tiles of 2x64 pixels
     default: *TCo = 64; *TK = 64; *BKM = 128; break;
   }
 }
@@ -638,7 +810,9 @@ extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, in
   const int K = first ? 64 : ksize * ksize * Cin;
   const char* force = getenv("CANNET_WGRAD_CFG");
   int cfg;
+  const bool halo_ok = !first && ksize == 3 && (Cout == 64 || Cout == 128) && Cin % 64 == 0;
   if (first) cfg = 0;
+  else if (halo_ok && getenv("CANNET_NO_HALO") == nullptr && M >= 262144) cfg = 8;
   else if (Cout % 256 == 0 && K >= 2048) cfg = 7;
   else if (Cout % 256 == 0 && K >= 1024) cfg = 2;
   else if (Cout % 128 == 0 && K >= 2048) cfg = 6;
@@ -648,6 +822,15 @@ extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, in
   if (force && !first) cfg = atoi(force);
   int TCo, TK, BKM;
   wgrad_tile(cfg, &TCo, &TK, &BKM);
+  if (cfg == 8) {
+    // slices of whole 2x64-pixel tiles; the Python side passes N,H,W to the launcher,
+    // here only the slice count matters: ~2 blocks per CU worth of (ci tile, slice) pairs.
+    const int nci = (Cin / 64) * (Cout / 64);
+    int S = 512 / nci;
+    if (S < 1) S = 1;
+    *S_out = S; *mslice_out = 0; *cfg_out = cfg;
+    return 0;
+  }
   const int ntile = (Cout / TCo) * ((K + TK - 1) / TK);
   // whole rounds of co-resident blocks (no half-empty last round)
   int S = target_blocks / ntile;
@@ -694,6 +877,20 @@ extern "C" int can_conv_wgrad(const void* dy, const void* x, float* ws, float* w
     a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.ksize = ksize; a.dil = dil; a.M = N * H * W; a.K = K;
     a.S = S; a.mslice = mslice;
     a.fdW = make_fastdiv((uint32_t)W); a.fdH = make_fastdiv((uint32_t)H); a.fdC = make_fastdiv((uint32_t)Cin);
+    if (cfg == 8) {
+      if (ksize != 3 || dil != 1 || (Cout != 64 && Cout != 128) || Cin % 64) return -6;
+      HaloArgs h;
+      h.dy = a.dy; h.x = a.x; h.zero = a.zero; h.ws = ws; h.wsb = wsb_used;
+      h.N = N; h.H = H; h.W = W; h.Cin = Cin; h.Cout = Cout; h.K = K; h.S = S;
+      h.tiles_y = (H + 1) / 2; h.tiles_x = (W + 63) / 64; h.ntiles = N * h.tiles_y * h.tiles_x;
+      h.tiles_per_slice = (h.ntiles + S - 1) / S;
+      rc = launch_halo<64, 2>(h, s);   // Cout = 128 runs as two 64-channel co tiles
+      if (rc) return rc;
+      const int plane = K * Cout;
+      hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((plane + 63) / 64 + 1), dim3(256), 0, s, ws, wsb_used, dw, db, S,
+                         K, Cout, Cin, 9, 0, beta, scale);
+      return (int)hipGetLastError();
+    }
     switch (cfg) {
       case 1: if (Cout % 128) return -4; rc = launch_wgrad2<2, 2, 1, 4, 1, 2>(a, s); break;
       case 2: if (Cout % 256) return -4; rc = launch_wgrad2<4, 2, 1, 3, 1, 2>(a, s); break;

@@ -107,3 +107,23 @@ def test_conv_wgrad_first_layer():
     gw, gb = torch.autograd.grad(y, (wr, br), dy.float().permute(0, 3, 1, 2))
     _close(dw, gw, 1e-2)
     _close(db, gb, 1e-2)
+
+
+@pytest.mark.parametrize("n,h,w,ci,co", [(1, 256, 1024, 64, 64), (2, 181, 733, 128, 128), (1, 301, 900, 64, 128)])
+def test_conv_wgrad_halo_path(n, h, w, ci, co):
+    """Large-M, small-channel layers take the halo-tiled wgrad kernel (odd H, W not a multiple of 64 included)."""
+    from can_distributed_pytorch_amd.ops import _ext
+    from can_distributed_pytorch_amd.ops import conv as C
+    assert _ext.require().wgrad_plan(n * h * w, ci, co, 3, 0, 1024)[2] == 8
+    torch.manual_seed(5)
+    x = torch.randn(n, h, w, ci, device="cuda").to(torch.bfloat16)
+    dy = torch.randn(n, h, w, co, device="cuda").to(torch.bfloat16)
+    dw = torch.empty(co, ci, 3, 3, device="cuda")
+    db = torch.empty(co, device="cuda")
+    C.conv_wgrad(dy, x, dw, db, ksize=3, dil=1)
+    wr = torch.zeros(co, ci, 3, 3, device="cuda", requires_grad=True)
+    br = torch.zeros(co, device="cuda", requires_grad=True)
+    y = F.conv2d(x.float().permute(0, 3, 1, 2), wr, br, padding=1)
+    gw, gb = torch.autograd.grad(y, (wr, br), dy.float().permute(0, 3, 1, 2))
+    _close(dw, gw, 1e-2)
+    _close(db, gb, 1e-2)
