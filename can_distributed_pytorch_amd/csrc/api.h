@@ -39,6 +39,11 @@ int can_ctx_bwd_final(const void* dcat, const void* dc, const float* dave, const
 // density.hip
 int can_density_map(const float* pts, int n, int H, int W, float* sigma_ws, float* out, int max_r, void* stream);
 
+// preprocess.hip
+int can_preprocess_image(const void* img, int H0, int W0, int C, int flip, void* out, int Ho, int Wo, void* stream);
+int can_preprocess_density(const float* d, int H0, int W0, int flip, float* out, int Ho, int Wo, float mult,
+                           void* stream);
+
 #ifdef __cplusplus
 }
 #endif

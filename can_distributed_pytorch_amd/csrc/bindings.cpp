@@ -111,4 +111,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("density_map", [](uintptr_t pts, int n, int H, int W, uintptr_t sig, uintptr_t out, int max_r, uintptr_t st) {
     check(can_density_map((const float*)pts, n, H, W, (float*)sig, (float*)out, max_r, P(st)), "density_map");
   });
+  // ---- input pipeline
+  m.def("preprocess_image", [](uintptr_t img, int H0, int W0, int C, int flip, uintptr_t out, int Ho, int Wo,
+                               uintptr_t st) {
+    check(can_preprocess_image(P(img), H0, W0, C, flip, P(out), Ho, Wo, P(st)), "preprocess_image");
+  });
+  m.def("preprocess_density", [](uintptr_t d, int H0, int W0, int flip, uintptr_t out, int Ho, int Wo, float mult,
+                                 uintptr_t st) {
+    check(can_preprocess_density((const float*)d, H0, W0, flip, (float*)out, Ho, Wo, mult, P(st)),
+          "preprocess_density");
+  });
 }

@@ -36,7 +36,7 @@ def imread(path: str) -> np.ndarray:
 
 class CrowdDataset(Dataset):
     def __init__(self, img_root: str, gt_dmap_root: str, gt_downsample: int = 1, phase: str = "train",
-                 seed: Optional[int] = None):
+                 seed: Optional[int] = None, raw: bool = False):
         self.img_root = img_root
         self.gt_dmap_root = gt_dmap_root
         self.gt_downsample = max(1, int(gt_downsample))
@@ -45,6 +45,9 @@ class CrowdDataset(Dataset):
                                 if os.path.isfile(os.path.join(img_root, f)) and f.lower().endswith(IMG_EXT))
         self.n_samples = len(self.img_names)
         self._rng = random.Random(seed)
+        # raw=True: return (uint8 image, full-res density, flip) and let the GPU
+        # preprocess it (ops/preprocess.py) instead of resizing on the CPU
+        self.raw = raw
 
     def __len__(self):
         return self.n_samples
@@ -60,6 +63,12 @@ class CrowdDataset(Dataset):
         img = imread(os.path.join(self.img_root, name))
         dmap = np.load(self.gt_path(name))                       # allow_pickle=False (default)
         flip = self.phase == "train" and self._rng.randint(0, 1) == 1
+        if self.raw:
+            if img.dtype != np.uint8:
+                img = np.clip(np.asarray(img, dtype=np.float64) * (255.0 if img.dtype.kind == "f" else 1.0),
+                              0, 255).astype(np.uint8)
+            return torch.from_numpy(np.ascontiguousarray(img)), torch.from_numpy(
+                np.ascontiguousarray(dmap, dtype=np.float32)), flip
         im, dm = prepare_pair(img, dmap, self.gt_downsample, flip)
         return torch.from_numpy(np.ascontiguousarray(im)), torch.from_numpy(np.ascontiguousarray(dm))
 

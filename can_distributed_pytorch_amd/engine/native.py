@@ -80,7 +80,7 @@ class NativeStepper:
         ex = self.ex
         st = _ext.stream_ptr(self.device)
         b6, sv = ex.forward_features(img, save=True)
-        ex.workspace(img.shape[0], img.shape[2], img.shape[3])
+        ex.workspace(*ex.input_hw(img))
         loss, et, d_b6 = ex.head_train(b6, gt, self.grads)
         red = self.reducer
         if red is not None:

@@ -61,16 +61,18 @@ def train_one_epoch(model, optimizer, train_loader, device, epoch, log=None):
     return mean_loss.item()
 
 
-def train_one_epoch_native(stepper, train_loader, device, epoch, log=None, log_every: int = 20):
-    """Fused native step per batch (see engine/native.py)."""
+def train_one_epoch_native(stepper, train_loader, device, epoch, log=None, log_every: int = 20, prep=None):
+    """Fused native step per batch (see engine/native.py).  ``prep`` maps a raw
+    loader batch to (img, gt) on the device (GPU preprocessing)."""
     stepper.model.train()
     loader = _progress(train_loader, is_main_process())
     total = torch.zeros(1, device=device)
     n = 0
     t0 = time.perf_counter()
     imgs = 0
-    for step, (img, gt) in enumerate(loader):
-        loss = stepper.step(img, gt)          # already averaged over ranks? no: SUM of per-rank losses
+    for step, batch in enumerate(loader):
+        img, gt = prep(batch) if prep is not None else batch
+        loss = stepper.step(img, gt)          # SUM of the per-rank losses (averaged below)
         total += loss.reshape(1) / max(1, get_world_size())
         n += 1
         imgs += img.shape[0] * get_world_size()
@@ -94,12 +96,14 @@ def train_one_epoch_native(stepper, train_loader, device, epoch, log=None, log_e
 
 
 @torch.no_grad()
-def evaluate(model, test_loader, device, epoch, show_images=False, use_wandb=False, out_dir="checkpoints/temp"):
+def evaluate(model, test_loader, device, epoch, show_images=False, use_wandb=False, out_dir="checkpoints/temp",
+             prep=None):
     model.eval()
     mae = torch.zeros(1, device=device)
     loader = _progress(test_loader, is_main_process())
     index = random.randint(0, max(0, len(test_loader) - 1))
-    for step, (img, gt) in enumerate(loader):
+    for step, batch in enumerate(loader):
+        img, gt = prep(batch) if prep is not None else batch
         img, gt = img.to(device, non_blocking=True), gt.to(device, non_blocking=True)
         et = model(img)
         mae += torch.abs(et.sum() - gt.sum())
@@ -108,7 +112,10 @@ def evaluate(model, test_loader, device, epoch, show_images=False, use_wandb=Fal
                 loader.desc = f"[epoch {epoch}]"
             if show_images and step == index:
                 from ..utils.vis import save_overlays
-                paths = save_overlays(img[0], gt[0], et[0], epoch, out_dir)
+                im0 = img[0]
+                if im0.dim() == 3 and im0.shape[-1] == 4:          # NHWC4 bf16 -> CHW float
+                    im0 = im0[..., :3].float().permute(2, 0, 1)
+                paths = save_overlays(im0, gt[0], et[0], epoch, out_dir)
                 if use_wandb:
                     from ..utils.metrics import wandb_log_images
                     wandb_log_images(paths, epoch)

@@ -175,6 +175,11 @@ class CANNetExecutor:
         return y
 
     def _img(self, img):
+        if img.dim() == 4 and img.shape[-1] == 4 and img.dtype == BF16:
+            # already in the first layer's NHWC4 layout (ops/preprocess.py)
+            if img.shape[1] % 8 or img.shape[2] % 8:
+                raise ValueError("H, W must be multiples of 8")
+            return img.contiguous()
         if img.dim() != 4 or img.shape[1] != 3:
             raise ValueError("input must be [N,3,H,W]")
         n, _, h, w = img.shape
@@ -336,6 +341,13 @@ class CANNetExecutor:
     def _shape_from(sv):
         x0 = sv["front_in"][0]
         return x0.shape[0], x0.shape[1], x0.shape[2]
+
+    @staticmethod
+    def input_hw(img):
+        """(N, H, W) of an NCHW image batch or an NHWC4 prepacked batch."""
+        if img.dim() == 4 and img.shape[-1] == 4 and img.dtype == BF16:
+            return img.shape[0], img.shape[1], img.shape[2]
+        return img.shape[0], img.shape[2], img.shape[3]
 
     # ----------------------------------------------------------- training head
     def head_train(self, b6, gt, grads, gscale: float = 1.0, beta: float = 0.0):

@@ -1,0 +1,52 @@
+"""GPU input pipeline: decoded uint8 image + full-res density -> network inputs.
+
+Same result as CrowdDataset's CPU transform (data/transforms.py:prepare_pair,
+reference model/CrowdDataset.py:38-67) but computed by csrc/preprocess.hip
+on the GPU, writing the first conv layer's NHWC4 bf16 layout directly.
+"""
+from __future__ import annotations
+
+from typing import List, Sequence, Tuple
+
+import torch
+
+from . import _ext
+
+
+def preprocess_batch(images: Sequence[torch.Tensor], densities: Sequence[torch.Tensor], flips: Sequence[bool],
+                     device, downsample: int = 8) -> Tuple[torch.Tensor, torch.Tensor]:
+    """images: uint8 [H,W] / [H,W,C] (CPU or GPU), densities: fp32 [H,W].  All samples must
+    resize to the same (H//d*d, W//d*d).  Returns (x4 [N,Ho,Wo,4] bf16, gt [N,1,Ho/d,Wo/d] fp32)."""
+    C = _ext.require()
+    dev = torch.device(device)
+    n = len(images)
+    if not (n == len(densities) == len(flips)) or n == 0:
+        raise ValueError("images, densities and flips must have the same non-zero length")
+    h0, w0 = images[0].shape[:2]
+    ho, wo = (h0 // downsample) * downsample, (w0 // downsample) * downsample
+    x4 = torch.empty(n, ho, wo, 4, dtype=torch.bfloat16, device=dev)
+    gt = torch.empty(n, 1, ho // downsample, wo // downsample, dtype=torch.float32, device=dev)
+    st = _ext.stream_ptr(dev)
+    for i, (im, dm, fl) in enumerate(zip(images, densities, flips)):
+        if im.dtype != torch.uint8:
+            raise ValueError("images must be uint8 (decoded JPEG/PNG)")
+        hh, ww = im.shape[:2]
+        if (hh // downsample * downsample, ww // downsample * downsample) != (ho, wo):
+            raise ValueError("all samples of a batch must resize to the same shape")
+        im = im.to(dev, non_blocking=True).contiguous()
+        ch = 1 if im.dim() == 2 else im.shape[2]
+        dm = dm.to(dev, dtype=torch.float32, non_blocking=True).contiguous()
+        if tuple(dm.shape) != (hh, ww):
+            raise ValueError("density must match the image size")
+        C.preprocess_image(im.data_ptr(), hh, ww, ch, int(bool(fl)), x4[i].data_ptr(), ho, wo, st)
+        C.preprocess_density(dm.data_ptr(), hh, ww, int(bool(fl)), gt[i].data_ptr(), ho // downsample,
+                             wo // downsample, float(downsample * downsample), st)
+    return x4, gt
+
+
+class RawCollate:
+    """collate_fn for CrowdDataset(raw=True): keeps samples as lists (variable sizes allowed until preprocessing)."""
+
+    def __call__(self, batch: List):
+        imgs, dens, flips = zip(*batch)
+        return list(imgs), list(dens), list(flips)

@@ -176,3 +176,21 @@ def test_no_uninitialized_reads_poisoned_allocator():
         torch.cuda.synchronize()
     assert not torch.isnan(outs[1]).any()
     assert torch.equal(outs[0], outs[1])
+
+
+def test_gpu_preprocess_matches_cpu_transform():
+    """ops/preprocess (HIP) == data/transforms.prepare_pair (cv2 INTER_LINEAR semantics), incl. flip."""
+    import numpy as np
+    from can_distributed_pytorch_amd.data.transforms import prepare_pair
+    from can_distributed_pytorch_amd.ops.preprocess import preprocess_batch
+    rng = np.random.default_rng(8)
+    for (h, w, c) in [(77, 101, 3), (64, 96, 3), (50, 70, 1)]:
+        img = (rng.random((h, w, c) if c > 1 else (h, w)) * 255).astype(np.uint8)
+        dm = rng.random((h, w)).astype(np.float32)
+        for flip in (False, True):
+            ref_img, ref_gt = prepare_pair(img, dm, 8, flip)
+            x4, gt = preprocess_batch([torch.from_numpy(img)], [torch.from_numpy(dm)], [flip], "cuda")
+            got = x4[0, ..., :3].float().permute(2, 0, 1).cpu().numpy()
+            assert np.abs(got - ref_img).max() < 0.03          # bf16 storage of the normalised image
+            assert bool((x4[0, ..., 3] == 0).all())
+            assert np.abs(gt[0].cpu().numpy() - ref_gt).max() < 1e-3

@@ -75,12 +75,16 @@ def build_parser():
     p.add_argument("--log-jsonl", type=str, default="checkpoints/metrics.jsonl")
     p.add_argument("--vgg16", type=str, default="", help="local torchvision VGG-16 state_dict for the frontend (reference downloads it)")
     p.add_argument("--eval-every", type=int, default=1)
+    p.add_argument("--gpu-preprocess", type=str2bool, default=True,
+                   help="decode on CPU workers, resize/flip/normalise on the GPU (hip impl, real data)")
     return p
 
 
-def make_loaders(args, world, rank):
+def make_loaders(args, world, rank, raw=False):
     from torch.utils.data import DataLoader, DistributedSampler, BatchSampler
     from can_distributed_pytorch_amd.data import CrowdDataset, SyntheticCrowdDataset
+    from can_distributed_pytorch_amd.ops.preprocess import RawCollate
+    collate = RawCollate() if raw else None
     if args.synthetic:
         h, w = (int(v) for v in args.synthetic.lower().split("x"))
         train_ds = SyntheticCrowdDataset(args.synthetic_n, h, w, seed=args.seed)
@@ -88,17 +92,17 @@ def make_loaders(args, world, rank):
     else:
         r = args.data_root
         train_ds = CrowdDataset(os.path.join(r, "train_data", "images"), os.path.join(r, "train_data", "ground_truth"),
-                                gt_downsample=8, phase="train", seed=args.seed + rank)
+                                gt_downsample=8, phase="train", seed=args.seed + rank, raw=raw)
         test_ds = CrowdDataset(os.path.join(r, "test_data", "images"), os.path.join(r, "test_data", "ground_truth"),
-                               gt_downsample=8, phase="test")
+                               gt_downsample=8, phase="test", raw=raw)
     train_sampler = DistributedSampler(train_ds, num_replicas=world, rank=rank, shuffle=True, seed=args.seed)
     test_sampler = DistributedSampler(test_ds, num_replicas=world, rank=rank, shuffle=True, seed=args.seed)
     bs = BatchSampler(train_sampler, args.batch_size, drop_last=False)
     pin = torch.cuda.is_available()
     train_loader = DataLoader(train_ds, batch_sampler=bs, num_workers=args.num_workers, pin_memory=pin,
-                              persistent_workers=args.num_workers > 0)
+                              persistent_workers=args.num_workers > 0, collate_fn=collate)
     test_loader = DataLoader(test_ds, sampler=test_sampler, batch_size=args.batch_size, num_workers=args.num_workers,
-                             pin_memory=pin, shuffle=False)
+                             pin_memory=pin, shuffle=False, collate_fn=collate)
     return train_loader, test_loader, train_sampler, test_sampler
 
 
@@ -118,7 +122,12 @@ def main(args):
     if rank == 0:
         print(f"[train start {time.strftime('%Y.%m.%d %H:%M:%S')}] world {world} impl {args.impl} {args}")
 
-    train_loader, test_loader, train_sampler, test_sampler = make_loaders(args, world, rank)
+    raw = bool(args.gpu_preprocess and args.impl == "hip" and not args.synthetic)
+    train_loader, test_loader, train_sampler, test_sampler = make_loaders(args, world, rank, raw=raw)
+    prep = None
+    if raw:
+        from can_distributed_pytorch_amd.ops.preprocess import preprocess_batch
+        prep = lambda b: preprocess_batch(b[0], b[1], b[2], device)  # noqa: E731
 
     model = CANNet(vgg16_path=args.vgg16 or None, backend="hip" if args.impl == "hip" else "torch")
     if os.path.exists(args.init_checkpoint):
@@ -163,13 +172,13 @@ def main(args):
                     g["lr"] = base_lr * world * f
         t0 = time.perf_counter()
         if args.impl == "hip":
-            mean_loss = train_one_epoch_native(stepper, train_loader, device, epoch, log=log)
+            mean_loss = train_one_epoch_native(stepper, train_loader, device, epoch, log=log, prep=prep)
         else:
             mean_loss = train_one_epoch(net, stepper.opt, train_loader, device, epoch)
         t_train = time.perf_counter() - t0
         if (epoch + 1) % args.eval_every == 0 or epoch == args.epochs - 1:
             mae_sum = evaluate(net, test_loader, device, epoch, show_images=args.show and rank == 0,
-                               use_wandb=use_wandb, out_dir=os.path.join(args.checkpoint_dir, "temp"))
+                               use_wandb=use_wandb, out_dir=os.path.join(args.checkpoint_dir, "temp"), prep=prep)
         else:
             mae_sum = float("nan")
         if rank == 0:
