@@ -111,3 +111,22 @@ def _hook_case(rank, world):
 
 def test_reducer_autograd_hooks_gloo():
     _run(_hook_case, 2)
+
+
+def _consistency_case(rank, world):
+    from can_distributed_pytorch_amd.parallel.consistency import check_replicas_consistent
+    x = torch.arange(1000, dtype=torch.float32)
+    assert check_replicas_consistent(x)
+    y = x.clone()
+    if rank == 1:
+        y[17] += 1e-3
+    try:
+        check_replicas_consistent(y)
+        raised = False
+    except RuntimeError:
+        raised = True
+    assert raised
+
+
+def test_replica_desync_detection_gloo():
+    _run(_consistency_case, 2)

@@ -75,6 +75,7 @@ def build_parser():
     p.add_argument("--log-jsonl", type=str, default="checkpoints/metrics.jsonl")
     p.add_argument("--vgg16", type=str, default="", help="local torchvision VGG-16 state_dict for the frontend (reference downloads it)")
     p.add_argument("--eval-every", type=int, default=1)
+    p.add_argument("--check-sync-every", type=int, default=1, help="epochs between cross-rank weight fingerprint checks (0: off)")
     p.add_argument("--gpu-preprocess", type=str2bool, default=True,
                    help="decode on CPU workers, resize/flip/normalise on the GPU (hip impl, real data)")
     return p
@@ -181,6 +182,13 @@ def main(args):
                                use_wandb=use_wandb, out_dir=os.path.join(args.checkpoint_dir, "temp"), prep=prep)
         else:
             mae_sum = float("nan")
+        if args.check_sync_every and (epoch + 1) % args.check_sync_every == 0 and world > 1:
+            from can_distributed_pytorch_amd.parallel.consistency import check_replicas_consistent, check_comm_health
+            if args.impl == "hip":
+                check_comm_health(stepper.reducer)
+                check_replicas_consistent(stepper.arena.data)
+            else:
+                check_replicas_consistent(torch.cat([p.detach().reshape(-1) for p in stepper.model.parameters()]))
         if rank == 0:
             mean_mae = mae_sum / test_sampler.total_size      # padded size, reference parity (Q6)
             if mean_mae < min_mae:
