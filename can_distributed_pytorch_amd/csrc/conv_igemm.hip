@@ -306,6 +306,60 @@ struct ConvArgs2 {
   FastDiv fdW, fdH;
 };
 
+// Shared epilogue of the LDS-DMA kernels: lane (fr, fq) of wave (wc, wp) owns
+// 16 consecutive output channels of one pixel per 16x16 pixel fragment.
+template <int WC, int WP, int PW, int EPI>
+__device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4][4 * PW], int ct, int pt,
+                                              int wc, int wp, int fr, int fq) {
+  constexpr int TC = 64 * WC, TP = 64 * PW * WP;
+  const int chb = ct * TC + wc * 64 + fq * 16;
+  float bias[16];
+  if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS) {
+#pragma unroll
+    for (int c = 0; c < 16; c += 4) {
+      const float4 b4 = *reinterpret_cast<const float4*>(a.bias + chb + c);
+      bias[c] = b4.x; bias[c + 1] = b4.y; bias[c + 2] = b4.z; bias[c + 3] = b4.w;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4 * PW; ++i) {
+    const int m = pt * TP + wp * 64 * PW + i * 16 + fr;
+    if (m >= a.M) continue;
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[j * 4 + r] = acc[j][i][r];
+    if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        v[c] += bias[c];
+        if (EPI == EPI_BIAS_RELU) v[c] = fmaxf(v[c], 0.f);
+      }
+    }
+    if (EPI == EPI_SIGMOID) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) v[c] = 1.f / (1.f + __expf(-v[c]));
+    }
+    const size_t off = (size_t)m * a.Cout + chb;
+    if (EPI == EPI_MASK) {
+      const uint4 m0 = *reinterpret_cast<const uint4*>(a.mask + off);
+      const uint4 m1 = *reinterpret_cast<const uint4*>(a.mask + off + 8);
+      const unsigned mw[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const unsigned short bits = (unsigned short)(mw[c >> 1] >> ((c & 1) * 16));
+        const bool pos = ((bits & 0x8000u) == 0) && ((bits & 0x7fffu) != 0);
+        v[c] = pos ? v[c] : 0.f;
+      }
+    }
+    *reinterpret_cast<uint4*>(a.y + off) =
+        make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
+    *reinterpret_cast<uint4*>(a.y + off + 8) =
+        make_uint4(pack2bf(v[8], v[9]), pack2bf(v[10], v[11]), pack2bf(v[12], v[13]), pack2bf(v[14], v[15]));
+  }
+}
+
 template <int WC, int WP, int PW, int EPI>
 __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds_kernel(ConvArgs2 a) {
   constexpr int NW = WC * WP;
@@ -402,53 +456,185 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds_kernel(ConvArgs2 a)
     }
   }
 
-  // ---- epilogue (same lane ownership as conv_igemm_kernel)
-  const int chb = ct * TC + wc * 64 + fq * 16;
-  float bias[16];
-  if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS) {
+  glds_epilogue<WC, WP, PW, EPI>(a, acc, ct, pt, wc, wp, fr, fq);
+}
+
+// ===========================================================================
+// v2 of the LDS-DMA kernel (same tiles, LDS image and epilogue):
+//  * per-lane DMA addressing hoisted out of the K loop: each B (pixel) DMA
+//    row keeps a 32-bit element offset and a 9-bit "tap in range" mask, the
+//    per-stage part (tap shift, channel chunk) is wave-uniform scalar math —
+//    no division or bounds arithmetic per stage;
+//  * the A (weight) and B DMA instructions are split at compile time (no
+//    uniform branches between DMA issues);
+//  * fragment reads are software-pipelined across the barrier: the second
+//    K half of stage s is read while the first half's MFMAs run, and the
+//    first half of stage s+1 is read (right after the barrier) while the
+//    second half's MFMAs run, so LDS read latency is never exposed at the
+//    head of an MFMA burst.
+// ===========================================================================
+template <int WC, int WP, int PW, int EPI>
+__global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a) {
+  constexpr int NW = WC * WP;
+  constexpr int TC = 64 * WC, TP = 64 * PW * WP;
+  constexpr int A_BYTES = TC * 128, B_BYTES = TP * 128;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int NIA = A_BYTES / 1024, NIB = B_BYTES / 1024;
+  constexpr int GA = NIA / NW, GB = NIB / NW;
+  static_assert(NIA % NW == 0 && NIB % NW == 0, "instruction split");
+
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wave % WC, wp = wave / WC;
+
+  const int nct = a.Cout / TC;
+  const int npt = (a.M + TP - 1) / TP;
+  const int tile = xcd_remap(blockIdx.x, nct * npt);
+  const int ct = tile % nct, pt = tile / nct;
+  const int Ktot = a.ksize * a.ksize * a.Cin;
+  const int nk = a.ksize * a.ksize * (a.Cin >> 6);
+  const int lc8 = ((lane & 7) ^ (lane >> 3)) * 8;     // swizzled 16-B chunk, in elements
+
+  int aoff[GA];
 #pragma unroll
-    for (int c = 0; c < 16; c += 4) {
-      const float4 b4 = *reinterpret_cast<const float4*>(a.bias + chb + c);
-      bias[c] = b4.x; bias[c + 1] = b4.y; bias[c + 2] = b4.z; bias[c + 3] = b4.w;
-    }
+  for (int j = 0; j < GA; ++j) {
+    const int r = (wave + NW * j) * 8 + (lane >> 3);
+    aoff[j] = (ct * TC + perm_row(r)) * Ktot + lc8;
   }
+  int boff[GB];
+  unsigned bmask[GB];
 #pragma unroll
-  for (int i = 0; i < 4 * PW; ++i) {
-    const int m = pt * TP + wp * 64 * PW + i * 16 + fr;
-    if (m >= a.M) continue;
-    float v[16];
+  for (int j = 0; j < GB; ++j) {
+    const int r = (wave + NW * j) * 8 + (lane >> 3);
+    const int m = pt * TP + r;
+    unsigned msk = 0;
+    if (m < a.M) {
+      const uint32_t q = fdiv((uint32_t)m, a.fdW);
+      const int ow = m - (int)q * a.W;
+      const int oh = (int)q - (int)fdiv(q, a.fdH) * a.H;
+      if (a.ksize == 3) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[j * 4 + r] = acc[j][i][r];
-    if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS) {
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        v[c] += bias[c];
-        if (EPI == EPI_BIAS_RELU) v[c] = fmaxf(v[c], 0.f);
+        for (int t = 0; t < 9; ++t) {
+          const int ih = oh + (t / 3 - 1) * a.dil, iw = ow + (t % 3 - 1) * a.dil;
+          if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) msk |= 1u << t;
+        }
+      } else {
+        msk = 1u;
       }
     }
-    if (EPI == EPI_SIGMOID) {
-#pragma unroll
-      for (int c = 0; c < 16; ++c) v[c] = 1.f / (1.f + __expf(-v[c]));
-    }
-    const size_t off = (size_t)m * a.Cout + chb;
-    if (EPI == EPI_MASK) {
-      const uint4 m0 = *reinterpret_cast<const uint4*>(a.mask + off);
-      const uint4 m1 = *reinterpret_cast<const uint4*>(a.mask + off + 8);
-      const unsigned mw[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        const unsigned short bits = (unsigned short)(mw[c >> 1] >> ((c & 1) * 16));
-        const bool pos = ((bits & 0x8000u) == 0) && ((bits & 0x7fffu) != 0);
-        v[c] = pos ? v[c] : 0.f;
-      }
-    }
-    *reinterpret_cast<uint4*>(a.y + off) =
-        make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
-    *reinterpret_cast<uint4*>(a.y + off + 8) =
-        make_uint4(pack2bf(v[8], v[9]), pack2bf(v[10], v[11]), pack2bf(v[12], v[13]), pack2bf(v[14], v[15]));
+    boff[j] = m * a.Cin + lc8;
+    bmask[j] = msk;
   }
+
+  // stage -> (tap, channel chunk) advanced incrementally (scalar)
+  int i_tap = 0, i_c0 = 0, i_k = 0;
+  auto issue = [&](int buf) {
+    int sh = 0;
+    if (a.ksize == 3) {
+      const int kh = (i_tap * 11) >> 5;
+      sh = ((kh - 1) * a.W + (i_tap - kh * 3 - 1)) * a.dil * a.Cin;
+    }
+    sh += i_c0;
+    unsigned char* sbase = smem + buf * STAGE;
+#pragma unroll
+    for (int j = 0; j < GA; ++j)
+      __builtin_amdgcn_global_load_lds(a.w + aoff[j] + i_k, (__attribute__((address_space(3))) void*)(sbase + (wave + NW * j) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+      const void* src = ((bmask[j] >> i_tap) & 1u) ? (const void*)(a.x + boff[j] + sh) : (const void*)a.zero;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sbase + A_BYTES + (wave + NW * j) * 1024), 16, 0, 0);
+    }
+    i_k += 64;
+    i_c0 += 64;
+    if (i_c0 == a.Cin) { i_c0 = 0; ++i_tap; }
+  };
+
+  f32x4 acc[4][4 * PW];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4 * PW; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  auto read = [&](int buf, int kk, bf16x8_t (&af)[4], bf16x8_t (&bfr)[4 * PW]) {
+    const uint4* As = reinterpret_cast<const uint4*>(smem + buf * STAGE);
+    const uint4* Bs = reinterpret_cast<const uint4*>(smem + buf * STAGE + A_BYTES);
+    const int chunk = kk * 4 + fq;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = wc * 64 + j * 16 + fr;
+      af[j] = __builtin_bit_cast(bf16x8_t, As[row * 8 + swz(row, chunk)]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4 * PW; ++i) {
+      const int row = wp * 64 * PW + i * 16 + fr;
+      bfr[i] = __builtin_bit_cast(bf16x8_t, Bs[row * 8 + swz(row, chunk)]);
+    }
+  };
+  // MFMAs over pixel fragments [i0, i1) (so the B fragments die in halves)
+  auto mma = [&](const bf16x8_t (&af)[4], const bf16x8_t (&bfr)[4 * PW], int i0, int i1) {
+#pragma unroll
+    for (int i = i0; i < i1; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], bfr[i], acc[j][i], 0, 0, 0);
+  };
+
+  bf16x8_t a0[4], b0[4 * PW], a1[4], b1[4 * PW];
+  issue(0);
+  if (nk > 1) {
+    issue(1);
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" :: "n"(GA + GB) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  read(0, 0, a0, b0);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  for (int s = 0; s < nk - 1; ++s) {
+    const int buf = s & 1;
+    read(buf, 1, a1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(a0, b0, 0, 4 * PW);
+    // this wave's reads of stage s are in registers, stage s+1 has landed
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0x0070);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (s + 2 < nk) issue(buf);
+    __builtin_amdgcn_sched_barrier(0);
+    // half of the second-half MFMAs first (their operands are complete, so
+    // any counter wait the compiler places here is free), then the reads of
+    // stage s+1's first half, hidden behind the other half
+    mma(a1, b1, 0, 2 * PW);
+    __builtin_amdgcn_sched_barrier(0);
+    read(buf ^ 1, 0, a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(a1, b1, 2 * PW, 4 * PW);
+    // the first-half reads have long landed; a visible lgkmcnt(0) keeps the
+    // compiler's counter model exact at the loop head
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+  }
+  read((nk - 1) & 1, 1, a1, b1);
+  mma(a0, b0, 0, 4 * PW);
+  mma(a1, b1, 0, 4 * PW);
+  glds_epilogue<WC, WP, PW, EPI>(a, acc, ct, pt, wc, wp, fr, fq);
+}
+
+template <int WC, int WP, int PW, int EPI>
+static int launch_glds2(const ConvArgs2& a, hipStream_t s) {
+  constexpr int TC = 64 * WC, TP = 64 * PW * WP;
+  const size_t lds = 2 * (size_t)(TC + TP) * 128;
+  auto kfn = conv_glds2_kernel<WC, WP, PW, EPI>;
+  static bool attr = false;
+  if (!attr) {
+    CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  const int nct = a.Cout / TC, npt = (a.M + TP - 1) / TP;
+  hipLaunchKernelGGL(kfn, dim3(nct * npt), dim3(64 * WC * WP), lds, s, a);
+  return (int)hipGetLastError();
 }
 
 template <int WC, int WP, int PW, int EPI>
@@ -474,6 +660,9 @@ static int dispatch_glds(const ConvArgs2& a, int tile_cfg, hipStream_t s) {
     case 11: if (a.Cout % 256) return -8; return launch_glds<4, 2, 2, EPI>(a, s);
     case 12: if (a.Cout % 128) return -8; return launch_glds<2, 4, 1, EPI>(a, s);
     case 13: return launch_glds<1, 8, 1, EPI>(a, s);
+    case 21: if (a.Cout % 256) return -8; return launch_glds2<4, 2, 2, EPI>(a, s);
+    case 22: if (a.Cout % 128) return -8; return launch_glds2<2, 4, 1, EPI>(a, s);
+    case 23: return launch_glds2<1, 8, 1, EPI>(a, s);
   }
   return -9;
 }

@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--layers", default="")
     ap.add_argument("--no-ref", action="store_true")
     ap.add_argument("--json", default="")
+    ap.add_argument("--tile", type=int, default=0, help="forced fwd/dgrad tile config (0 = auto)")
     a = ap.parse_args()
     dev = "cuda"
     out = []
@@ -61,8 +62,11 @@ def main():
         dw = torch.empty_like(wt)
         db = torch.empty(co, device=dev)
         res = {"layer": name, "shape": [n, h, w, ci, co, dil], "gflop": fl / 1e9}
-        res["fwd_ms"] = timeit(lambda: C.conv_igemm(x, wf, b, ksize=3, dil=dil))
-        res["dgrad_ms"] = timeit(lambda: C.conv_igemm(dy, wd, None, ksize=3, dil=dil, epi=C.EPI_MASK, mask=x)) \
+        # --tile >= 20: the v2 kernel with the tile that fits the channel count
+        pick = (lambda c: (21 if c % 256 == 0 else 22 if c % 128 == 0 else 23) if a.tile >= 20 else a.tile)
+        t, td = pick(co), pick(ci)
+        res["fwd_ms"] = timeit(lambda: C.conv_igemm(x, wf, b, ksize=3, dil=dil, tile=t))
+        res["dgrad_ms"] = timeit(lambda: C.conv_igemm(dy, wd, None, ksize=3, dil=dil, epi=C.EPI_MASK, mask=x, tile=td)) \
             if ci == co or True else 0
         res["wgrad_ms"] = timeit(lambda: C.conv_wgrad(dy, x, dw, db, ksize=3, dil=dil, ws=ws))
         if not a.no_ref:

@@ -28,6 +28,10 @@ def _close(a, b, tol=2e-2):
     (1, 20, 20, 128, 256, 3, 1, 4),
     (1, 20, 20, 128, 256, 3, 1, 11), (1, 20, 20, 128, 256, 3, 1, 12), (1, 20, 20, 128, 256, 3, 1, 13),
     (2, 9, 13, 64, 128, 3, 2, 0), (1, 7, 5, 512, 1024, 3, 2, 0), (3, 11, 17, 64, 64, 3, 1, 0),
+    # v2 pipelined LDS-DMA kernel: every tile, 1x1 (nk = Cin/64), nk = 1, nk = 2, dilation 2, ragged M
+    (1, 20, 20, 128, 256, 3, 1, 21), (1, 20, 20, 128, 256, 3, 1, 22), (1, 20, 20, 128, 256, 3, 1, 23),
+    (2, 16, 24, 512, 512, 1, 1, 21), (1, 9, 13, 64, 256, 1, 1, 21), (1, 9, 13, 128, 128, 1, 1, 22),
+    (2, 32, 32, 256, 512, 3, 2, 21), (3, 11, 17, 64, 64, 3, 1, 23), (2, 9, 13, 64, 128, 3, 2, 22),
 ])
 def test_conv_fwd(n, h, w, ci, co, k, dil, tile):
     from can_distributed_pytorch_amd.ops import conv as C
@@ -53,8 +57,10 @@ def test_conv_first_layer():
     _close(y, ref)
 
 
-@pytest.mark.parametrize("n,h,w,ci,co,dil", [(2, 24, 40, 64, 128, 1), (1, 16, 16, 512, 1024, 2), (1, 9, 13, 64, 64, 1)])
-def test_conv_dgrad_mask(n, h, w, ci, co, dil):
+@pytest.mark.parametrize("n,h,w,ci,co,dil,tile", [
+    (2, 24, 40, 64, 128, 1, 0), (1, 16, 16, 512, 1024, 2, 0), (1, 9, 13, 64, 64, 1, 0),
+    (1, 16, 16, 512, 1024, 2, 21), (2, 24, 40, 128, 64, 1, 22), (1, 9, 13, 64, 64, 1, 23)])
+def test_conv_dgrad_mask(n, h, w, ci, co, dil, tile):
     """dX = conv_transpose(dY, W) * (mask > 0) via the same kernel with the flipped pack."""
     from can_distributed_pytorch_amd.ops import conv as C
     torch.manual_seed(2)
@@ -62,7 +68,7 @@ def test_conv_dgrad_mask(n, h, w, ci, co, dil):
     wt = (torch.randn(co, ci, 3, 3, device=dev) * 0.05).to(torch.bfloat16).float()
     dy = torch.randn(n, h, w, co, device=dev).to(torch.bfloat16)
     mask = torch.randn(n, h, w, ci, device=dev).to(torch.bfloat16)
-    dx = C.conv_igemm(dy, C.pack_weight_dgrad(wt), None, ksize=3, dil=dil, epi=C.EPI_MASK, mask=mask)
+    dx = C.conv_igemm(dy, C.pack_weight_dgrad(wt), None, ksize=3, dil=dil, epi=C.EPI_MASK, mask=mask, tile=tile)
     xr = torch.zeros(n, ci, h, w, device=dev, requires_grad=True)
     y = F.conv2d(xr, wt, None, padding=dil, dilation=dil)
     (gx,) = torch.autograd.grad(y, xr, dy.float().permute(0, 3, 1, 2))

@@ -139,3 +139,24 @@ def test_train_py_two_rank_gloo(tmp_path):
                          str(tmp_path / "epoch_0.pth"), "--device", "cpu"], capture_output=True, text=True,
                         timeout=300)
     assert r2.returncode == 0 and "mae:" in r2.stdout, r2.stderr[-2000:]
+
+
+def test_module_smoke_mains():
+    """Reference smoke tests C09 / C11: `python model/CANNet.py`, `python model/CrowdDataset.py`."""
+    for mod in ("model/CANNet.py", "model/CrowdDataset.py"):
+        r = subprocess.run([sys.executable, os.path.join(ROOT, mod)], capture_output=True, text=True, timeout=300,
+                           cwd=ROOT, env=dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES=""))
+        assert r.returncode == 0 and r.stdout.strip(), (mod, r.stderr[-2000:])
+
+
+def test_train_py_batch_norm_variant(tmp_path):
+    """make_layers(batch_norm=True) variant through train.py (stock path); BN keys land in the checkpoint."""
+    cmd = [sys.executable, os.path.join(ROOT, "train.py"), "--device", "cpu", "--synthetic", "32x48",
+           "--synthetic-n", "4", "--epochs", "1", "--batch-size", "2", "--num-workers", "0", "--wandb", "false",
+           "--show", "false", "--batch-norm", "true", "--checkpoint-dir", str(tmp_path),
+           "--log-jsonl", str(tmp_path / "m.jsonl")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=str(tmp_path),
+                       env=dict(os.environ, OMP_NUM_THREADS="2"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    sd = torch.load(tmp_path / "epoch_0.pth", map_location="cpu", weights_only=True)
+    assert "frontend.1.running_mean" in sd and "backend.1.weight" in sd

@@ -52,7 +52,9 @@ def build_parser():
     p.add_argument("--batch-size", type=int, default=1)
     p.add_argument("--lr", type=float, default=1e-7)
     p.add_argument("--lrf", type=float, default=0.1, help="final lr factor for --lr-schedule cosine (unused otherwise, as in the reference)")
-    p.add_argument("--syncBN", type=str2bool, default=True, help="accepted for compatibility; CANNet has no BN layers (no-op)")
+    p.add_argument("--syncBN", type=str2bool, default=True,
+                   help="convert BatchNorm to SyncBatchNorm when world > 1 (the reference model has no BN: a no-op "
+                        "unless --batch-norm)")
     p.add_argument("--wandb", type=str2bool, default=True, help="log to wandb if it is installed")
     p.add_argument("--show", type=str2bool, default=True, help="save GT/prediction overlay PNGs each epoch")
     p.add_argument("--data_root", type=str, default="./data/Shanghai_part_A/")
@@ -76,6 +78,8 @@ def build_parser():
     p.add_argument("--vgg16", type=str, default="", help="local torchvision VGG-16 state_dict for the frontend (reference downloads it)")
     p.add_argument("--eval-every", type=int, default=1)
     p.add_argument("--check-sync-every", type=int, default=1, help="epochs between cross-rank weight fingerprint checks (0: off)")
+    p.add_argument("--batch-norm", type=str2bool, default=False,
+                   help="make_layers(batch_norm=True) variant (reference C04 branch; stock autograd path only)")
     p.add_argument("--gpu-preprocess", type=str2bool, default=True,
                    help="decode on CPU workers, resize/flip/normalise on the GPU (hip impl, real data)")
     return p
@@ -115,6 +119,9 @@ def main(args):
     if args.impl == "hip" and not use_gpu:
         print("[no GPU: falling back to --impl torch on CPU]")
         args.impl = "torch"
+    if args.batch_norm and args.impl == "hip":
+        print("[--batch-norm: the fused native step has no BN layers; using --impl torch]")
+        args.impl = "torch"
     base_lr = args.lr
     torch.manual_seed(args.seed)
     os.makedirs(args.checkpoint_dir, exist_ok=True)
@@ -130,7 +137,10 @@ def main(args):
         from can_distributed_pytorch_amd.ops.preprocess import preprocess_batch
         prep = lambda b: preprocess_batch(b[0], b[1], b[2], device)  # noqa: E731
 
-    model = CANNet(vgg16_path=args.vgg16 or None, backend="hip" if args.impl == "hip" else "torch")
+    model = CANNet(vgg16_path=args.vgg16 or None, backend="hip" if args.impl == "hip" else "torch",
+                   batch_norm=args.batch_norm)
+    if args.syncBN and world > 1 and args.batch_norm:
+        model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model)      # train.py:116-118
     if os.path.exists(args.init_checkpoint):
         res = load_checkpoint(model, args.init_checkpoint, strict=False)
         if rank == 0:
