@@ -539,7 +539,7 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
     unsigned char* sbase = smem + buf * STAGE;
 #pragma unroll
     for (int j = 0; j < GA; ++j)
-      __builtin_amdgcn_global_load_lds(a.w + aoff[j] + i_k, (__attribute__((address_space(3))) void*)(sbase + (wave + NW * j) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(a.w + aoff[j] + i_k), (__attribute__((address_space(3))) void*)(sbase + (wave + NW * j) * 1024), 16, 0, 0);
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
       const void* src = ((bmask[j] >> i_tap) & 1u) ? (const void*)(a.x + boff[j] + sh) : (const void*)a.zero;

@@ -160,3 +160,15 @@ def test_train_py_batch_norm_variant(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     sd = torch.load(tmp_path / "epoch_0.pth", map_location="cpu", weights_only=True)
     assert "frontend.1.running_mean" in sd and "backend.1.weight" in sd
+
+
+def test_native_extension_links():
+    """The in-tree _C extension (when built) must load: catches kernels whose host stub was
+    silently dropped (undefined symbol at import) before anything reaches a GPU box."""
+    import glob
+    so = glob.glob(os.path.join(ROOT, "can_distributed_pytorch_amd", "_C*.so"))
+    if not so:
+        pytest.skip("native extension not built here")
+    import importlib
+    C = importlib.import_module("can_distributed_pytorch_amd._C")
+    assert C.arch() and hasattr(C, "conv_igemm") and hasattr(C, "conv_wgrad")
