@@ -655,7 +655,7 @@ static int launch_glds(const ConvArgs2& a, hipStream_t s) {
 template <int EPI>
 static int dispatch_glds(const ConvArgs2& a, int tile_cfg, hipStream_t s) {
   int cfg = tile_cfg;
-  if (cfg == 0) cfg = (a.Cout % 256 == 0) ? 11 : (a.Cout % 128 == 0) ? 12 : 13;
+  if (cfg == 0) cfg = (a.Cout % 256 == 0) ? 21 : (a.Cout % 128 == 0) ? 22 : 23;   // v2 (pipelined) by default
   switch (cfg) {
     case 11: if (a.Cout % 256) return -8; return launch_glds<4, 2, 2, EPI>(a, s);
     case 12: if (a.Cout % 128) return -8; return launch_glds<2, 4, 1, EPI>(a, s);

@@ -536,6 +536,246 @@ static int launch_wgrad2(const WgradArgs2& a, hipStream_t s) {
 }
 
 // ===========================================================================
+// v2 of the LDS-DMA weight-gradient kernel for row-aligned layers
+// (W % 64 == 0, K % TK == 0): every 64-pixel stage lies inside ONE image row,
+// so a stage is (n, oh, ow0..ow0+63) and every per-lane quantity of the DMA
+// addressing — the lane's (tap, ci) and its row inside the stage — is a
+// loop invariant.  Per stage the wave computes (oh, ow0) once (scalar) and
+// each B (activation) DMA costs two range compares and a select; the dY
+// DMA is a pure pointer add.  Fragment reads are software-pipelined across
+// the barrier exactly like conv_glds2_kernel (second K half read under the
+// first half's MFMAs, the next stage's first half read right after the
+// barrier under the other half).
+// ===========================================================================
+template <int WC, int WK, int KW>
+__global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2 a) {
+  constexpr int NW = WC * WK;
+  constexpr int TCo = 64 * WC, TK = 64 * WK * KW;
+  constexpr int BKM = 64;                          // pixels per stage (2 MFMA K steps)
+  constexpr int RBA = TCo * 2, RBB = TK * 2;
+  constexpr int A_BYTES = BKM * RBA, B_BYTES = BKM * RBB;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int NIA = A_BYTES / 1024, NIB = B_BYTES / 1024;
+  constexpr int GA = NIA / NW, GB = NIB / NW;
+  static_assert(NIA % NW == 0 && NIB % NW == 0, "instruction split");
+  static_assert(RBB == 512, "B row = 256 k (2 rows per 1-KiB DMA)");
+
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wave % WC, wk = wave / WC;
+
+  const int nco = a.Cout / TCo, nkt = a.K / TK;
+  const int ntile = nco * nkt;
+  const int nbias = (a.wsb != nullptr) ? a.S : 0;
+
+  // ---- bias blocks (first in the grid, so they overlap the GEMM blocks):
+  // db partial of one pixel slice = column sums of dY, plain loads + VALU
+  if ((int)blockIdx.x < nbias) {
+    const int slice = blockIdx.x;
+    const int mbeg = slice * a.mslice, mend = min(a.M, mbeg + a.mslice);
+    const int cg = tid & 63, rg = tid >> 6;      // 8-channel group, row group (NW row groups)
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (cg * 8 < a.Cout) {
+      const bf16_t* base = a.dy + cg * 8;
+      int m = mbeg + rg;
+      for (; m + 3 * NW < mend; m += 4 * NW) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const uint4*>(base + (size_t)(m + u * NW) * a.Cout);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const unsigned w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+          for (int e2 = 0; e2 < 4; ++e2) {
+            s[2 * e2] += __uint_as_float(w4[e2] << 16);
+            s[2 * e2 + 1] += __uint_as_float(w4[e2] & 0xffff0000u);
+          }
+        }
+      }
+      for (; m < mend; m += NW) {
+        const uint4 v = *reinterpret_cast<const uint4*>(base + (size_t)m * a.Cout);
+        const unsigned w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e2 = 0; e2 < 4; ++e2) {
+          s[2 * e2] += __uint_as_float(w4[e2] << 16);
+          s[2 * e2 + 1] += __uint_as_float(w4[e2] & 0xffff0000u);
+        }
+      }
+    }
+    float* red = reinterpret_cast<float*>(smem);   // [NW][64][8]
+#pragma unroll
+    for (int e2 = 0; e2 < 8; ++e2) red[(rg * 64 + cg) * 8 + e2] = s[e2];
+    __syncthreads();
+    if (rg == 0 && cg * 8 < a.Cout) {
+#pragma unroll
+      for (int e2 = 0; e2 < 8; ++e2) {
+        float t = 0.f;
+        for (int r = 0; r < NW; ++r) t += red[(r * 64 + cg) * 8 + e2];
+        a.wsb[(size_t)slice * a.Cout + cg * 8 + e2] = t;
+      }
+    }
+    return;
+  }
+
+  const int bid = xcd_remap(blockIdx.x - nbias, ntile * a.S);
+  const int tile = bid % ntile, slice = bid / ntile;
+  const int co0 = (tile % nco) * TCo, k0 = (tile / nco) * TK;
+  const int mbeg = slice * a.mslice;
+  const int mend = min(a.M, mbeg + a.mslice);
+  const int nstage = (mend > mbeg) ? (mend - mbeg) / BKM : 0;   // M, mslice multiples of 64
+
+  // dY tile through a buffer resource: per-lane 32-bit offsets, stage base in soffset
+  const __amdgpu_buffer_rsrc_t dy_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, (short)0, a.M * a.Cout * 2, 0x00020000);
+  unsigned aoff[GA];
+#pragma unroll
+  for (int j = 0; j < GA; ++j) {
+    const int byte = (wave + NW * j) * 1024 + lane * 16;
+    const int row = byte / RBA;
+    const int lc16 = swz8b<RBA>(row, ((byte % RBA) / 16) * 2) >> 1;
+    aoff[j] = (unsigned)(row * a.Cout + co0 + lc16 * 8) * 2u;
+  }
+  // Cin % TK == 0: the whole k tile is ONE tap -> (dh, dw) are block-uniform
+  const int tap = k0 / a.Cin;
+  int dh = 0, dw = 0;
+  if (a.ksize == 3) {
+    const int kh = (tap * 11) >> 5;
+    dh = (kh - 1) * a.dil;
+    dw = (tap - kh * 3 - 1) * a.dil;
+  }
+  const int ci0 = k0 - tap * a.Cin;
+  const int lrow = lane >> 5;
+  int boff[GB];
+#pragma unroll
+  for (int j = 0; j < GB; ++j) {
+    const int byte = (wave + NW * j) * 1024 + lane * 16;
+    const int row = byte / RBB;
+    const int lc16 = swz8b<RBB>(row, ((byte % RBB) / 16) * 2) >> 1;
+    boff[j] = (row + dh * a.W + dw) * a.Cin + ci0 + lc16 * 8;
+  }
+
+  auto issue = [&](int st, int buf) {
+    const int m0 = mbeg + st * BKM;
+    const uint32_t q = fdiv((uint32_t)m0, a.fdW);
+    const int ow0 = m0 - (int)q * a.W;
+    const int oh = (int)q - (int)fdiv(q, a.fdH) * a.H;
+    const bool row_ok = (unsigned)(oh + dh) < (unsigned)a.H;     // stage-uniform
+    unsigned char* sbase = smem + buf * STAGE;
+    const unsigned soff = (unsigned)m0 * (unsigned)a.Cout * 2u;
+#pragma unroll
+    for (int j = 0; j < GA; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(dy_rsrc, (__attribute__((address_space(3))) void*)(sbase + (wave + NW * j) * 1024),
+                                               16, (int)aoff[j], (int)soff, 0, 0);
+    const bf16_t* xs = a.x + (size_t)m0 * a.Cin;
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+      const int iw = ow0 + dw + 2 * (wave + NW * j) + lrow;
+      const bool ok = row_ok && ((unsigned)iw < (unsigned)a.W);
+      const void* src = ok ? (const void*)(xs + boff[j]) : (const void*)a.zero;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sbase + A_BYTES + (wave + NW * j) * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[4][4 * KW];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4 * KW; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, qd = (lane & 15) >> 2, p = lane & 3;
+  auto rd = [&](const unsigned char* base, int rb_wide, int rb, int prow0, int col0) -> bf16x8_t {
+    const int r0 = prow0 + 8 * g + qd;
+    const int c8 = (col0 >> 2) + p;
+    const int s0 = rb_wide ? swz8b<256>(r0, c8) : swz8b<128>(r0, c8);
+    const int s1 = rb_wide ? swz8b<256>(r0 + 4, c8) : swz8b<128>(r0 + 4, c8);
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + r0 * rb + s0 * 8));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + (r0 + 4) * rb + s1 * 8));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8_t, v);
+  };
+  auto read = [&](int buf, int kk, bf16x8_t (&af)[4], bf16x8_t (&bfr)[4 * KW]) {
+    const unsigned char* Ab = smem + buf * STAGE;
+    const unsigned char* Bb = Ab + A_BYTES;
+    const int prow0 = kk * 32;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) af[j] = rd(Ab, RBA >= 256, RBA, prow0, wc * 64 + j * 16);
+#pragma unroll
+    for (int i = 0; i < 4 * KW; ++i) bfr[i] = rd(Bb, RBB >= 256, RBB, prow0, wk * 64 * KW + i * 16);
+  };
+  auto mma = [&](const bf16x8_t (&af)[4], const bf16x8_t (&bfr)[4 * KW], int i0, int i1) {
+#pragma unroll
+    for (int i = i0; i < i1; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], bfr[i], acc[j][i], 0, 0, 0);
+  };
+
+  if (nstage > 0) {
+    bf16x8_t a0[4], b0[4 * KW], a1[4], b1[4 * KW];
+    issue(0, 0);
+    if (nstage > 1) {
+      issue(1, 1);
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" :: "n"(GA + GB) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    read(0, 0, a0, b0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    for (int st = 0; st < nstage - 1; ++st) {
+      const int buf = st & 1;
+      read(buf, 1, a1, b1);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(a0, b0, 0, 4 * KW);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_waitcnt(0x0070);
+      asm volatile("s_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (st + 2 < nstage) issue(st + 2, buf);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(a1, b1, 0, 2 * KW);
+      __builtin_amdgcn_sched_barrier(0);
+      read(buf ^ 1, 0, a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(a1, b1, 2 * KW, 4 * KW);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+    }
+    read((nstage - 1) & 1, 1, a1, b1);
+    mma(a0, b0, 0, 4 * KW);
+    mma(a1, b1, 0, 4 * KW);
+  }
+
+  const int fr = lane & 15, fq = lane >> 4;
+  float* slab = a.ws + (size_t)slice * a.K * a.Cout;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4 * KW; ++i) {
+      const int k = k0 + wk * 64 * KW + i * 16 + fr;
+      const int co = co0 + wc * 64 + j * 16 + fq * 4;
+      *reinterpret_cast<f32x4*>(slab + (size_t)k * a.Cout + co) = acc[j][i];
+    }
+}
+
+template <int WC, int WK, int KW>
+static int launch_wgrad3(const WgradArgs2& a, hipStream_t s) {
+  constexpr int STAGE = 64 * (64 * WC + 64 * WK * KW) * 2;
+  const size_t lds = 2 * (size_t)STAGE;
+  auto kfn = wgrad_glds2_kernel<WC, WK, KW>;
+  static bool attr = false;
+  if (!attr) {
+    CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  const int ntile = (a.Cout / (64 * WC)) * (a.K / (64 * WK * KW));
+  const int nbias = (a.wsb != nullptr) ? a.S : 0;
+  hipLaunchKernelGGL(kfn, dim3(nbias + ntile * a.S), dim3(64 * WC * WK), lds, s, a);
+  return (int)hipGetLastError();
+}
+
+// ===========================================================================
 // Halo-tiled weight gradient for 3x3 / dilation-1 layers with Cin % 64 == 0 and
 // Cout in {64, 128} (the high-resolution VGG layers conv1_2, conv2_1, conv2_2).
 //
@@ -800,6 +1040,7 @@ static void wgrad_tile(int cfg, int* TCo, int* TK, int* BKM) {
     case 5: *TCo = 256; *TK = 256; *BKM = 32; break;
     case 6: *TCo = 128; *TK = 256; *BKM = 64; break;
     case 7: *TCo = 256; *TK = 256; *BKM = 64; break;
+    case 9: *TCo = 256; *TK = 256; *BKM = 64; break;   // v2 (row-aligned layers), falls back to 7
     case 8: *TCo = 0; *TK = 0; *BKM = 128; break;   // halo kernel: tiles of 2x64 pixels
     default: *TCo = 64; *TK = 64; *BKM = 128; break;
   }
@@ -813,7 +1054,7 @@ extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, in
   const bool halo_ok = !first && ksize == 3 && (Cout == 64 || Cout == 128) && Cin % 64 == 0;
   if (first) cfg = 0;
   else if (halo_ok && getenv("CANNET_NO_HALO") == nullptr && M >= 262144) cfg = 8;
-  else if (Cout % 256 == 0 && K >= 2048) cfg = 7;
+  else if (Cout % 256 == 0 && K >= 2048) cfg = (K % 256 == 0 && getenv("CANNET_WGRAD_V1") == nullptr) ? 9 : 7;
   else if (Cout % 256 == 0 && K >= 1024) cfg = 2;
   else if (Cout % 128 == 0 && K >= 2048) cfg = 6;
   else if (Cout % 128 == 0) cfg = 1;
@@ -834,6 +1075,22 @@ extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, in
   const int ntile = (Cout / TCo) * ((K + TK - 1) / TK);
   // whole rounds of co-resident blocks (no half-empty last round)
   int S = target_blocks / ntile;
+  if ((cfg == 7 || cfg == 9) && getenv("CANNET_WGRAD_MANY_SLICES") == nullptr) {
+    // 8-wave 256x256 kernels run one block per CU: as few pixel slices as fill
+    // whole rounds of the CUs to >= 90 % (fewer fp32 partial slabs to write and
+    // reduce, longer K loops per block)
+    static int ncu = 0;
+    if (!ncu) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+        ncu = 256;
+    }
+    for (int R = 1; R <= 8; ++R) {
+      const int s = (ncu * R) / ntile;
+      if (s >= 1 && (long long)ntile * s * 10 >= 9LL * ncu * R) { S = s; break; }
+    }
+  }
   if (S < 1) S = 1;
   const int max_s = (M + BKM - 1) / BKM;
   if (S > max_s) S = max_s;
@@ -899,6 +1156,13 @@ extern "C" int can_conv_wgrad(const void* dy, const void* x, float* ws, float* w
       case 5: if (Cout % 256) return -4; rc = launch_wgrad2<4, 2, 1, 4, 2, 1>(a, s); break;
       case 6: if (Cout % 128) return -4; rc = launch_wgrad2<2, 2, 1, 3, 2, 2>(a, s); break;
       case 7: if (Cout % 256) return -4; rc = launch_wgrad2<4, 2, 1, 2, 2, 2>(a, s); break;
+      case 9:
+        if (Cout % 256) return -4;
+        if (W % 64 == 0 && Cin % 256 == 0 && mslice % 64 == 0 && (long long)a.M * Cout * 2 < 0x7fffffffLL)
+          rc = launch_wgrad3<4, 2, 2>(a, s);
+        else
+          rc = launch_wgrad2<4, 2, 1, 2, 2, 2>(a, s);   // same tiles / slicing as cfg 7
+        break;
       default: return -5;
     }
   }

@@ -98,6 +98,29 @@ def test_conv_wgrad(n, h, w, ci, co, k, dil):
     _close(db, gb, 1e-2)
 
 
+@pytest.mark.parametrize("n,h,w,ci,co,dil,bias", [
+    (1, 6, 64, 256, 256, 1, True), (2, 5, 128, 512, 256, 2, True), (1, 3, 64, 1024, 512, 2, True),
+    (3, 4, 64, 256, 512, 1, False), (1, 1, 64, 512, 512, 2, True)])
+def test_conv_wgrad_v2_row_aligned(n, h, w, ci, co, dil, bias):
+    """W % 64 == 0, Cin % 256 == 0 layers take the v2 pipelined wgrad (cfg 9) with bias column-sum blocks."""
+    from can_distributed_pytorch_amd.ops import _ext
+    from can_distributed_pytorch_amd.ops import conv as C
+    assert _ext.require().wgrad_plan(n * h * w, ci, co, 3, 0, 1024)[2] == 9
+    torch.manual_seed(6)
+    x = torch.randn(n, h, w, ci, device="cuda").to(torch.bfloat16)
+    dy = torch.randn(n, h, w, co, device="cuda").to(torch.bfloat16)
+    dw = torch.empty(co, ci, 3, 3, device="cuda")
+    db = torch.empty(co, device="cuda") if bias else None
+    C.conv_wgrad(dy, x, dw, db, ksize=3, dil=dil)
+    wr = torch.zeros(co, ci, 3, 3, device="cuda", requires_grad=True)
+    br = torch.zeros(co, device="cuda", requires_grad=True)
+    y = F.conv2d(x.float().permute(0, 3, 1, 2), wr, br, padding=dil, dilation=dil)
+    gw, gb = torch.autograd.grad(y, (wr, br), dy.float().permute(0, 3, 1, 2))
+    _close(dw, gw, 1e-2)
+    if bias:
+        _close(db, gb, 1e-2)
+
+
 def test_conv_wgrad_first_layer():
     from can_distributed_pytorch_amd.ops import conv as C
     torch.manual_seed(4)
