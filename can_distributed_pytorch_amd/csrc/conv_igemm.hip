@@ -637,6 +637,177 @@ static int launch_glds2(const ConvArgs2& a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// ===========================================================================
+// Halo-tiled 3x3 / dilation-1 conv for Cin = 64 (conv1_2 fwd + dgrad, conv2_1
+// fwd: the 768x1024 / 384x512 layers).  The generic kernel streams the
+// activation once per tap (9x re-reads, ~7 GB of LDS-DMA for conv1_2 at
+// batch 8); here a block stages the (4+2) x (128+2) input halo of its
+// 4 x 128 output tile ONCE (97.5 KB, XOR-swizzled per pixel; conflict-free
+// for any column shift) and every tap reads its shifted window from it.
+// Weights stream per tap through a 3-slot LDS ring (tap t+2 loads while tap t
+// computes).  Waves: CO = 64 -> 8 waves = 4 rows x 2 column halves (64 co x
+// 64 px each); CO = 128 -> 8 waves = 4 rows x 2 channel halves (64 co x 128 px).
+// ===========================================================================
+struct HaloConvArgs {
+  const bf16_t* x;
+  const bf16_t* w;      // packed [CO][9*64] (fwd or dgrad pack)
+  const float* bias;
+  const bf16_t* mask;
+  bf16_t* y;
+  const bf16_t* zero;
+  int N, H, W, tiles_x, tiles_y;
+};
+
+template <int CO, int EPI>
+__global__ void __launch_bounds__(512, 1) conv_halo64_kernel(HaloConvArgs a) {
+  constexpr int TR = 4, TCOL = 128, HR = TR + 2, HC = TCOL + 2;
+  constexpr int HPIX = HR * HC;                       // 780 halo pixels
+  constexpr int NHI = (HPIX + 7) / 8;                 // 98 one-KiB DMA pieces
+  constexpr int HALO_BYTES = NHI * 1024;
+  constexpr int WTAP = CO * 128;                      // one tap of weights: CO rows x 64 ci
+  constexpr int GW = WTAP / 1024 / 8;                 // weight DMA pieces per wave per tap
+  constexpr int PW = CO / 64;                         // pixel fragments per wave / 4
+  static_assert(GW >= 1, "weights split");
+
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* halo = smem;
+  unsigned char* wring = smem + HALO_BYTES;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  const int ntile = a.N * a.tiles_y * a.tiles_x;
+  const int tile = xcd_remap(blockIdx.x, ntile);
+  const int tx = tile % a.tiles_x;
+  const int ty = (tile / a.tiles_x) % a.tiles_y;
+  const int n = tile / (a.tiles_x * a.tiles_y);
+  const int oh0 = ty * TR, ow0 = tx * TCOL;
+
+  // ---- halo DMA (once): piece i covers halo pixels 8i..8i+7
+  for (int i = wave; i < NHI; i += 8) {
+    const int hp = i * 8 + (lane >> 3);
+    const int hr = hp / HC, hc = hp - hr * HC;
+    const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
+    const void* src = a.zero;
+    if (hp < HPIX && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+      src = a.x + ((size_t)(n * a.H + ih) * a.W + iw) * 64 + (((lane & 7) ^ (hp & 7)) * 8);
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(halo + i * 1024), 16, 0, 0);
+  }
+  auto issue_w = [&](int t) {
+    unsigned char* dst = wring + (t % 3) * WTAP;
+#pragma unroll
+    for (int j = 0; j < GW; ++j) {
+      const int r = (wave + 8 * j) * 8 + (lane >> 3);
+      const int lc = (lane & 7) ^ (r & 7);
+      __builtin_amdgcn_global_load_lds((const void*)(a.w + (size_t)perm_row(r) * 576 + t * 64 + lc * 8),
+                                       (__attribute__((address_space(3))) void*)(dst + (wave + 8 * j) * 1024), 16, 0, 0);
+    }
+  };
+  issue_w(0);
+  issue_w(1);
+
+  // wave -> (row, co half / column half)
+  const int r = wave >> 1;
+  const int wc = (CO == 128) ? (wave & 1) : 0;
+  const int colbase = (CO == 128) ? 0 : (wave & 1) * 64;
+  f32x4 acc[4][4 * PW];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4 * PW; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int t = 0; t < 9; ++t) {
+    // tap t's weights (and, for t = 0, the halo) have landed; the ring slot of
+    // tap t-1 is free once every wave is past this barrier
+    if (t + 1 < 9) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" :: "n"(GW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    if (t + 2 < 9) issue_w(t + 2);
+    const int kh = (t * 11) >> 5, kw = t - kh * 3;
+    const uint4* As = reinterpret_cast<const uint4*>(wring + (t % 3) * WTAP);
+    const uint4* Hs = reinterpret_cast<const uint4*>(halo);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = kk * 4 + fq;
+      bf16x8_t af[4], bfr[4 * PW];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = wc * 64 + j * 16 + fr;
+        af[j] = __builtin_bit_cast(bf16x8_t, As[row * 8 + swz(row, chunk)]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4 * PW; ++i) {
+        const int hp = (r + kh) * HC + colbase + i * 16 + fr + kw;
+        bfr[i] = __builtin_bit_cast(bf16x8_t, Hs[hp * 8 + (chunk ^ (hp & 7))]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4 * PW; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], bfr[i], acc[j][i], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue: lane owns 16 consecutive channels of one pixel per fragment
+  const int oh = oh0 + r;
+  if (oh >= a.H) return;
+  const int chb = wc * 64 + fq * 16;
+  float bias[16];
+  if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS) {
+#pragma unroll
+    for (int c = 0; c < 16; c += 4) {
+      const float4 b4 = *reinterpret_cast<const float4*>(a.bias + chb + c);
+      bias[c] = b4.x; bias[c + 1] = b4.y; bias[c + 2] = b4.z; bias[c + 3] = b4.w;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4 * PW; ++i) {
+    const int ow = ow0 + colbase + i * 16 + fr;
+    if (ow >= a.W) continue;
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[j * 4 + q] = acc[j][i][q];
+    if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        v[c] += bias[c];
+        if (EPI == EPI_BIAS_RELU) v[c] = fmaxf(v[c], 0.f);
+      }
+    }
+    const size_t off = ((size_t)(n * a.H + oh) * a.W + ow) * CO + chb;
+    if (EPI == EPI_MASK) {
+      const uint4 m0 = *reinterpret_cast<const uint4*>(a.mask + off);
+      const uint4 m1 = *reinterpret_cast<const uint4*>(a.mask + off + 8);
+      const unsigned mw[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const unsigned short bits = (unsigned short)(mw[c >> 1] >> ((c & 1) * 16));
+        const bool pos = ((bits & 0x8000u) == 0) && ((bits & 0x7fffu) != 0);
+        v[c] = pos ? v[c] : 0.f;
+      }
+    }
+    *reinterpret_cast<uint4*>(a.y + off) =
+        make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
+    *reinterpret_cast<uint4*>(a.y + off + 8) =
+        make_uint4(pack2bf(v[8], v[9]), pack2bf(v[10], v[11]), pack2bf(v[12], v[13]), pack2bf(v[14], v[15]));
+  }
+}
+
+template <int CO, int EPI>
+static int launch_halo64(const HaloConvArgs& a, hipStream_t s) {
+  constexpr int HALO_BYTES = ((6 * 130 + 7) / 8) * 1024;
+  const size_t lds = HALO_BYTES + 3 * (size_t)CO * 128;
+  auto kfn = conv_halo64_kernel<CO, EPI>;
+  static bool attr = false;
+  if (!attr) {
+    CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  hipLaunchKernelGGL(kfn, dim3(a.N * a.tiles_y * a.tiles_x), dim3(512), lds, s, a);
+  return (int)hipGetLastError();
+}
+
 template <int WC, int WP, int PW, int EPI>
 static int launch_glds(const ConvArgs2& a, hipStream_t s) {
   constexpr int TC = 64 * WC, TP = 64 * PW * WP;
@@ -695,6 +866,22 @@ extern "C" int can_conv_igemm(const void* x, const void* w, const float* bias, c
   if (first) {
     CAN_EPI_CASE(LOAD_FIRST, EPI_BIAS_RELU)
     return -5;
+  }
+  if (tile_cfg == 31) {
+    // halo-tiled Cin = 64 kernel (explicit; see conv_halo64_kernel)
+    if (Cin != 64 || ksize != 3 || dil != 1 || (Cout != 64 && Cout != 128)) return -11;
+    HaloConvArgs h;
+    h.x = a.x; h.w = a.w; h.bias = a.bias; h.mask = a.mask; h.y = a.y; h.zero = conv_zero_page();
+    if (!h.zero) return -10;
+    h.N = N; h.H = H; h.W = W; h.tiles_x = (W + 127) / 128; h.tiles_y = (H + 3) / 4;
+#define CAN_HALO_CASE(E) \
+    if (epi == E) return (Cout == 64) ? launch_halo64<64, E>(h, s) : launch_halo64<128, E>(h, s);
+    CAN_HALO_CASE(EPI_BIAS_RELU)
+    CAN_HALO_CASE(EPI_MASK)
+    CAN_HALO_CASE(EPI_NONE)
+    CAN_HALO_CASE(EPI_BIAS)
+#undef CAN_HALO_CASE
+    return -6;
   }
   if (tile_cfg == 0 || tile_cfg >= 10) {
     if (H < 2 || W < 2) return -7;

@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--layers", default="")
     ap.add_argument("--no-ref", action="store_true")
     ap.add_argument("--json", default="")
+    ap.add_argument("--halo", action="store_true", help="halo-tiled kernel for the Cin=64 fwd / Cout=64 dgrad layers")
     ap.add_argument("--tile", type=int, default=0, help="forced fwd/dgrad tile config (0 = auto)")
     a = ap.parse_args()
     dev = "cuda"
@@ -65,6 +66,10 @@ def main():
         # --tile >= 20: the v2 kernel with the tile that fits the channel count
         pick = (lambda c: (21 if c % 256 == 0 else 22 if c % 128 == 0 else 23) if a.tile >= 20 else a.tile)
         t, td = pick(co), pick(ci)
+        if a.halo and ci == 64 and dil == 1 and co in (64, 128):
+            t = 31
+        if a.halo and co == 64 and dil == 1 and ci in (64, 128):
+            td = 31
         res["fwd_ms"] = timeit(lambda: C.conv_igemm(x, wf, b, ksize=3, dil=dil, tile=t))
         res["dgrad_ms"] = timeit(lambda: C.conv_igemm(dy, wd, None, ksize=3, dil=dil, epi=C.EPI_MASK, mask=x, tile=td)) \
             if ci == co or True else 0

@@ -32,6 +32,9 @@ def _close(a, b, tol=2e-2):
     (1, 20, 20, 128, 256, 3, 1, 21), (1, 20, 20, 128, 256, 3, 1, 22), (1, 20, 20, 128, 256, 3, 1, 23),
     (2, 16, 24, 512, 512, 1, 1, 21), (1, 9, 13, 64, 256, 1, 1, 21), (1, 9, 13, 128, 128, 1, 1, 22),
     (2, 32, 32, 256, 512, 3, 2, 21), (3, 11, 17, 64, 64, 3, 1, 23), (2, 9, 13, 64, 128, 3, 2, 22),
+    # halo-tiled Cin = 64 kernel: full tiles, ragged rows / columns, Cout 64 and 128
+    (1, 4, 128, 64, 64, 3, 1, 31), (2, 10, 200, 64, 64, 3, 1, 31), (1, 9, 130, 64, 128, 3, 1, 31),
+    (2, 3, 7, 64, 128, 3, 1, 31),
 ])
 def test_conv_fwd(n, h, w, ci, co, k, dil, tile):
     from can_distributed_pytorch_amd.ops import conv as C
@@ -59,7 +62,8 @@ def test_conv_first_layer():
 
 @pytest.mark.parametrize("n,h,w,ci,co,dil,tile", [
     (2, 24, 40, 64, 128, 1, 0), (1, 16, 16, 512, 1024, 2, 0), (1, 9, 13, 64, 64, 1, 0),
-    (1, 16, 16, 512, 1024, 2, 21), (2, 24, 40, 128, 64, 1, 22), (1, 9, 13, 64, 64, 1, 23)])
+    (1, 16, 16, 512, 1024, 2, 21), (2, 24, 40, 128, 64, 1, 22), (1, 9, 13, 64, 64, 1, 23),
+    (2, 9, 140, 64, 64, 1, 31), (1, 12, 256, 128, 64, 1, 31)])
 def test_conv_dgrad_mask(n, h, w, ci, co, dil, tile):
     """dX = conv_transpose(dY, W) * (mask > 0) via the same kernel with the flipped pack."""
     from can_distributed_pytorch_amd.ops import conv as C
