@@ -77,38 +77,47 @@ __device__ __forceinline__ void bil(int S, int x, int L, int& x0, int& x1, float
 // rowacc[n][y][bin][c] = sum_x wx(bin, x) * in_S(bin)[n][y][x][c]
 // POOL: one input (fv) for all scales.  BILINEAR: per scale the sum of two
 // inputs (sdir_S + dc_S), in[2*S_idx] and in[2*S_idx+1], each [P][C].
+// Block = one image row (n, y) x 64 channel groups of 8; the row is split in 4
+// column segments over adjacent lanes (thread = cg*4 + seg), the 4 partial
+// sums are combined with lane shuffles (fixed order), and each lane stores 3
+// of the 12 bins.  The 12 x w bin weights are tabulated once per block in LDS.
 template <bool POOL>
 __global__ void __launch_bounds__(256) ctx_rows_kernel(const uint4* __restrict__ in0, const uint4* __restrict__ sdir,
                                                        const uint4* __restrict__ dc, float* __restrict__ rowacc,
                                                        int N, int h, int w, int C) {
+  extern __shared__ float wtab[];                  // [12][w]
   const int C8 = C >> 3;
   const size_t P = (size_t)N * h * w;
-  const size_t total = (size_t)N * h * C8;   // one thread per (n, y, 8-channel group)
-  for (size_t t = blockIdx.x * 256 + threadIdx.x; t < total; t += (size_t)gridDim.x * 256) {
-    const int cg = t % C8;
-    const size_t ny = t / C8;                 // n*h + y
-    float acc[12][8];
+  const int ncgb = (C8 + 63) / 64;
+  const size_t ny = blockIdx.x / ncgb;             // n*h + y
+  const int cg = (blockIdx.x % ncgb) * 64 + (threadIdx.x >> 2);
+  const int seg = threadIdx.x & 3;
+  for (int i = threadIdx.x; i < 12 * w; i += 256) {
+    const int b = i / w, x = i - b * w;
+    const int si = (b >= 6) ? 3 : (b >= 3) ? 2 : (b >= 1) ? 1 : 0;
+    const int S = (si == 0) ? 1 : (si == 1) ? 2 : (si == 2) ? 3 : 6;
+    const int bo = (si == 0) ? 0 : (si == 1) ? 1 : (si == 2) ? 3 : 6;
+    wtab[i] = axis_w<POOL>(b - bo, S, x, w);
+  }
+  __syncthreads();
+  float acc[12][8];
 #pragma unroll
-    for (int b = 0; b < 12; ++b)
+  for (int b = 0; b < 12; ++b)
 #pragma unroll
-      for (int k = 0; k < 8; ++k) acc[b][k] = 0.f;
-    for (int x = 0; x < w; ++x) {
+    for (int k = 0; k < 8; ++k) acc[b][k] = 0.f;
+  const int xs = (w + 3) / 4;
+  const int x0 = seg * xs, x1 = min(w, x0 + xs);
+  if (cg < C8) {
+    for (int x = x0; x < x1; ++x) {
       const size_t pix = ny * w + x;
       if (POOL) {
         float v[8];
         unpack8c(in0[pix * C8 + cg], v);
 #pragma unroll
-        for (int si = 0; si < 4; ++si) {
-          const int S = (si == 0) ? 1 : (si == 1) ? 2 : (si == 2) ? 3 : 6;
-          const int bo = (si == 0) ? 0 : (si == 1) ? 1 : (si == 2) ? 3 : 6;
+        for (int b = 0; b < 12; ++b) {
+          const float wt = wtab[b * w + x];
 #pragma unroll
-          for (int j = 0; j < 6; ++j) {
-            if (j < S) {
-              const float wt = axis_w<true>(j, S, x, w);
-#pragma unroll
-              for (int k = 0; k < 8; ++k) acc[bo + j][k] += wt * v[k];
-            }
-          }
+          for (int k = 0; k < 8; ++k) acc[b][k] += wt * v[k];
         }
       } else {
 #pragma unroll
@@ -123,7 +132,7 @@ __global__ void __launch_bounds__(256) ctx_rows_kernel(const uint4* __restrict__
 #pragma unroll
           for (int j = 0; j < 6; ++j) {
             if (j < S) {
-              const float wt = axis_w<false>(j, S, x, w);
+              const float wt = wtab[(bo + j) * w + x];
 #pragma unroll
               for (int k = 0; k < 8; ++k) acc[bo + j][k] += wt * v[k];
             }
@@ -131,11 +140,25 @@ __global__ void __launch_bounds__(256) ctx_rows_kernel(const uint4* __restrict__
         }
       }
     }
+  }
+  // combine the 4 segments (lanes seg 0..3 of one channel group), fixed order
+#pragma unroll
+  for (int b = 0; b < 12; ++b)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float t = acc[b][k];
+      t += __shfl_xor(t, 1);
+      t += __shfl_xor(t, 2);
+      acc[b][k] = t;
+    }
+  if (cg < C8) {
     float* o = rowacc + (ny * 12) * C + cg * 8;
 #pragma unroll
     for (int b = 0; b < 12; ++b) {
-      *reinterpret_cast<float4*>(o + (size_t)b * C) = make_float4(acc[b][0], acc[b][1], acc[b][2], acc[b][3]);
-      *reinterpret_cast<float4*>(o + (size_t)b * C + 4) = make_float4(acc[b][4], acc[b][5], acc[b][6], acc[b][7]);
+      if (b % 4 == seg) {
+        *reinterpret_cast<float4*>(o + (size_t)b * C) = make_float4(acc[b][0], acc[b][1], acc[b][2], acc[b][3]);
+        *reinterpret_cast<float4*>(o + (size_t)b * C + 4) = make_float4(acc[b][4], acc[b][5], acc[b][6], acc[b][7]);
+      }
     }
   }
 }
@@ -189,28 +212,115 @@ __device__ __forceinline__ void up8(const float* __restrict__ T, int n, int si, 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Pixel-wise kernels.  Thread = (image row n*h+y, 8-channel group, one of 4
+// column segments); a wave covers 64 channel groups of the same pixels
+// (coalesced 1-KiB rows).  The row's y-interpolated cell values of all 12 bins
+// (RowTab) are built once per thread in registers and reused along the run of
+// pixels, so the bilinear upsample costs FMAs, not table reads.
+// ---------------------------------------------------------------------------
+struct RowTab {
+  float v[12][8];
+};
+
+// R[bin] = y-bilinear mix of the table T at row y (bins of scale S = cells (i, j), j < S)
+__device__ __forceinline__ void rowtab_bilinear(const float* __restrict__ T, int n, int y, int h, int C, int cg,
+                                                RowTab& R) {
+#pragma unroll
+  for (int si = 0; si < 4; ++si) {
+    const int S = (si == 0) ? 1 : (si == 1) ? 2 : (si == 2) ? 3 : 6;
+    const int bo = (si == 0) ? 0 : (si == 1) ? 1 : (si == 2) ? 3 : 6;
+    const int co = (si == 0) ? 0 : (si == 1) ? 1 : (si == 2) ? 5 : 14;
+    int y0, y1;
+    float ly;
+    bil(S, y, h, y0, y1, ly);
+    const float* base = T + ((size_t)n * 50 + co) * C + cg * 8;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      if (j < S) {
+        const float* p0 = base + (size_t)(y0 * S + j) * C;
+        const float* p1 = base + (size_t)(y1 * S + j) * C;
+#pragma unroll
+        for (int k = 0; k < 8; k += 4) {
+          const float4 a = *reinterpret_cast<const float4*>(p0 + k), b = *reinterpret_cast<const float4*>(p1 + k);
+          R.v[bo + j][k + 0] = (1.f - ly) * a.x + ly * b.x;
+          R.v[bo + j][k + 1] = (1.f - ly) * a.y + ly * b.y;
+          R.v[bo + j][k + 2] = (1.f - ly) * a.z + ly * b.z;
+          R.v[bo + j][k + 3] = (1.f - ly) * a.w + ly * b.w;
+        }
+      }
+    }
+  }
+}
+
+// u = x-bilinear of the row table, scale si, column x
+template <int SI>
+__device__ __forceinline__ void up_row(const RowTab& R, int x, int w, float* u) {
+  constexpr int S = (SI == 0) ? 1 : (SI == 1) ? 2 : (SI == 2) ? 3 : 6;
+  constexpr int BO = (SI == 0) ? 0 : (SI == 1) ? 1 : (SI == 2) ? 3 : 6;
+  int x0, x1;
+  float lx;
+  bil(S, x, w, x0, x1, lx);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) u[k] = 0.f;
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const float wj = ((j == x0) ? 1.f - lx : 0.f) + ((j == x1) ? lx : 0.f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) u[k] += wj * R.v[BO + j][k];
+  }
+}
+
+template <typename F>
+__device__ __forceinline__ void up_all(const RowTab& R, int x, int w, F&& f) {
+  float u[8];
+  up_row<0>(R, x, w, u); f(0, u);
+  up_row<1>(R, x, w, u); f(1, u);
+  up_row<2>(R, x, w, u); f(2, u);
+  up_row<3>(R, x, w, u); f(3, u);
+}
+
+struct RowRun {
+  size_t ny;   // n*h + y
+  int n, y, cg, x0, x1;
+  bool ok;
+};
+__device__ __forceinline__ RowRun row_run(int h, int w, int C8) {
+  RowRun r;
+  const int ncgb = (C8 + 63) / 64;
+  const int seg = blockIdx.x & 1;
+  const size_t rest = blockIdx.x >> 1;
+  r.ny = rest / ncgb;
+  r.cg = (int)(rest % ncgb) * 64 + (threadIdx.x & 63);
+  // 256 threads = 4 waves: wave = sub-segment of the block's column segment
+  const int xs = (w + 7) / 8;                      // 8 runs per row (2 blocks x 4 waves)
+  const int run = seg * 4 + (threadIdx.x >> 6);
+  r.x0 = run * xs;
+  r.x1 = min(w, r.x0 + xs);
+  r.n = (int)(r.ny / h);
+  r.y = (int)(r.ny - (size_t)r.n * h);
+  r.ok = r.cg < C8;
+  return r;
+}
+
 // c_S = up_S - fv for the 4 scales: cs[si][P][C] bf16
 __global__ void __launch_bounds__(256) ctx_expand_kernel(const uint4* __restrict__ fv, const float* __restrict__ T,
                                                          uint4* __restrict__ cs, int N, int h, int w, int C) {
   const int C8 = C >> 3;
-  const size_t P = (size_t)N * h * w;
-  const size_t total = P * C8;
-  for (size_t t = blockIdx.x * 256 + threadIdx.x; t < total; t += (size_t)gridDim.x * 256) {
-    const int cg = t % C8;
-    const size_t p = t / C8;
-    const int x = p % w;
-    const int y = (p / w) % h;
-    const int n = p / ((size_t)w * h);
+  const size_t total = (size_t)N * h * w * C8;
+  const RowRun r = row_run(h, w, C8);
+  if (!r.ok) return;
+  RowTab R;
+  rowtab_bilinear(T, r.n, r.y, h, C, r.cg, R);
+  for (int x = r.x0; x < r.x1; ++x) {
+    const size_t t = (r.ny * w + x) * C8 + r.cg;
     float f[8];
     unpack8c(fv[t], f);
-#pragma unroll
-    for (int si = 0; si < 4; ++si) {
-      float u[8];
-      up8(T, n, si, y, x, h, w, C, cg, u);
+    up_all(R, x, w, [&](int si, float* u) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) u[k] -= f[k];
       cs[(size_t)si * total + t] = pack8c(u);
-    }
+    });
   }
 }
 
@@ -219,29 +329,27 @@ __global__ void __launch_bounds__(256) ctx_fuse_kernel(const uint4* __restrict__
                                                        const float* __restrict__ T, uint4* __restrict__ cat, int N,
                                                        int h, int w, int C) {
   const int C8 = C >> 3;
-  const size_t P = (size_t)N * h * w;
-  const size_t total = P * C8;
-  for (size_t t = blockIdx.x * 256 + threadIdx.x; t < total; t += (size_t)gridDim.x * 256) {
-    const int cg = t % C8;
-    const size_t p = t / C8;
-    const int x = p % w;
-    const int y = (p / w) % h;
-    const int n = p / ((size_t)w * h);
+  const size_t total = (size_t)N * h * w * C8;
+  const RowRun r = row_run(h, w, C8);
+  if (!r.ok) return;
+  RowTab R;
+  rowtab_bilinear(T, r.n, r.y, h, C, r.cg, R);
+  for (int x = r.x0; x < r.x1; ++x) {
+    const size_t p = r.ny * w + x;
+    const size_t t = p * C8 + r.cg;
     float num[8], den[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) { num[k] = 0.f; den[k] = 0.f; }
-#pragma unroll
-    for (int si = 0; si < 4; ++si) {
-      float u[8], wv[8];
-      up8(T, n, si, y, x, h, w, C, cg, u);
+    up_all(R, x, w, [&](int si, float* u) {
+      float wv[8];
       unpack8c(ws[(size_t)si * total + t], wv);
 #pragma unroll
       for (int k = 0; k < 8; ++k) { num[k] += wv[k] * u[k]; den[k] += wv[k]; }
-    }
+    });
 #pragma unroll
     for (int k = 0; k < 8; ++k) num[k] = num[k] / (den[k] + 1e-12f);
-    cat[p * 2 * C8 + cg] = fv[t];
-    cat[p * 2 * C8 + C8 + cg] = pack8c(num);
+    cat[p * 2 * C8 + r.cg] = fv[t];
+    cat[p * 2 * C8 + C8 + r.cg] = pack8c(num);
   }
 }
 
@@ -250,25 +358,23 @@ __global__ void __launch_bounds__(256) ctx_bwd_e1_kernel(const uint4* __restrict
                                                          const float* __restrict__ T, uint4* __restrict__ dz,
                                                          uint4* __restrict__ sdir, int N, int h, int w, int C) {
   const int C8 = C >> 3;
-  const size_t P = (size_t)N * h * w;
-  const size_t total = P * C8;
-  for (size_t t = blockIdx.x * 256 + threadIdx.x; t < total; t += (size_t)gridDim.x * 256) {
-    const int cg = t % C8;
-    const size_t p = t / C8;
-    const int x = p % w;
-    const int y = (p / w) % h;
-    const int n = p / ((size_t)w * h);
+  const size_t total = (size_t)N * h * w * C8;
+  const RowRun r = row_run(h, w, C8);
+  if (!r.ok) return;
+  RowTab R;
+  rowtab_bilinear(T, r.n, r.y, h, C, r.cg, R);
+  for (int x = r.x0; x < r.x1; ++x) {
+    const size_t p = r.ny * w + x;
+    const size_t t = p * C8 + r.cg;
     float s[4][8], wv[4][8], num[8], den[8], dfi[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) { num[k] = 0.f; den[k] = 0.f; }
-#pragma unroll
-    for (int si = 0; si < 4; ++si) {
-      up8(T, n, si, y, x, h, w, C, cg, s[si]);
+    up_all(R, x, w, [&](int si, float* u) {
       unpack8c(ws[(size_t)si * total + t], wv[si]);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) { num[k] += wv[si][k] * s[si][k]; den[k] += wv[si][k]; }
-    }
-    unpack8c(dcat[p * 2 * C8 + C8 + cg], dfi);
+      for (int k = 0; k < 8; ++k) { s[si][k] = u[k]; num[k] += wv[si][k] * u[k]; den[k] += wv[si][k]; }
+    });
+    unpack8c(dcat[p * 2 * C8 + C8 + r.cg], dfi);
 #pragma unroll
     for (int k = 0; k < 8; ++k) { den[k] += 1e-12f; num[k] = num[k] / den[k]; }   // num := fi
 #pragma unroll
@@ -288,43 +394,63 @@ __global__ void __launch_bounds__(256) ctx_bwd_e1_kernel(const uint4* __restrict
 }
 
 // dfv = (dcat_fv - sum_S dc_S + sum_S pool^T(dave_S)) * (fv > 0)
+// pool^T: the row's pooled-cell gradients (bins containing y, divided by the
+// bin height) are summed once per thread into a RowTab; per column the bins
+// containing x contribute / bin width.
 __global__ void __launch_bounds__(256) ctx_bwd_final_kernel(const uint4* __restrict__ dcat,
                                                             const uint4* __restrict__ dc, const float* __restrict__ dave,
                                                             const uint4* __restrict__ fv, uint4* __restrict__ dfv,
                                                             int N, int h, int w, int C) {
   const int C8 = C >> 3;
-  const size_t P = (size_t)N * h * w;
-  const size_t total = P * C8;
-  for (size_t t = blockIdx.x * 256 + threadIdx.x; t < total; t += (size_t)gridDim.x * 256) {
-    const int cg = t % C8;
-    const size_t p = t / C8;
-    const int x = p % w;
-    const int y = (p / w) % h;
-    const int n = p / ((size_t)w * h);
+  const size_t total = (size_t)N * h * w * C8;
+  const RowRun r = row_run(h, w, C8);
+  if (!r.ok) return;
+  RowTab R;
+  int xs_[12], xe_[12];
+#pragma unroll
+  for (int si = 0; si < 4; ++si) {
+    const int S = (si == 0) ? 1 : (si == 1) ? 2 : (si == 2) ? 3 : 6;
+    const int bo = (si == 0) ? 0 : (si == 1) ? 1 : (si == 2) ? 3 : 6;
+    const int co = (si == 0) ? 0 : (si == 1) ? 1 : (si == 2) ? 5 : 14;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      if (j < S) {
+        int xs, xe;
+        pool_bin(j, S, w, xs, xe);
+        xs_[bo + j] = xs;
+        xe_[bo + j] = xe;
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < S; ++i) {
+          int ys, ye;
+          pool_bin(i, S, h, ys, ye);
+          if (r.y < ys || r.y >= ye) continue;
+          const float inv = 1.f / (float)((ye - ys) * (xe - xs));
+          const float* d = dave + ((size_t)r.n * 50 + co + i * S + j) * C + r.cg * 8;
+          const float4 a = *reinterpret_cast<const float4*>(d), b = *reinterpret_cast<const float4*>(d + 4);
+          acc[0] += a.x * inv; acc[1] += a.y * inv; acc[2] += a.z * inv; acc[3] += a.w * inv;
+          acc[4] += b.x * inv; acc[5] += b.y * inv; acc[6] += b.z * inv; acc[7] += b.w * inv;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) R.v[bo + j][k] = acc[k];
+      }
+    }
+  }
+  for (int x = r.x0; x < r.x1; ++x) {
+    const size_t p = r.ny * w + x;
+    const size_t t = p * C8 + r.cg;
     float g[8], u[8];
-    unpack8c(dcat[p * 2 * C8 + cg], g);
+    unpack8c(dcat[p * 2 * C8 + r.cg], g);
 #pragma unroll
     for (int si = 0; si < 4; ++si) {
       unpack8c(dc[(size_t)si * total + t], u);
 #pragma unroll
       for (int k = 0; k < 8; ++k) g[k] -= u[k];
-      const int S = kScale[si];
-      // bins containing (y, x): at most 2 per axis
-      for (int i = 0; i < S; ++i) {
-        int ys, ye;
-        pool_bin(i, S, h, ys, ye);
-        if (y < ys || y >= ye) continue;
-        for (int j = 0; j < S; ++j) {
-          int xs, xe;
-          pool_bin(j, S, w, xs, xe);
-          if (x < xs || x >= xe) continue;
-          const float inv = 1.f / (float)((ye - ys) * (xe - xs));
-          const float* d = dave + ((size_t)n * 50 + kCellOff[si] + i * S + j) * C + cg * 8;
-          const float4 a = *reinterpret_cast<const float4*>(d), b = *reinterpret_cast<const float4*>(d + 4);
-          g[0] += a.x * inv; g[1] += a.y * inv; g[2] += a.z * inv; g[3] += a.w * inv;
-          g[4] += b.x * inv; g[5] += b.y * inv; g[6] += b.z * inv; g[7] += b.w * inv;
-        }
-      }
+    }
+#pragma unroll
+    for (int b = 0; b < 12; ++b) {
+      const float m = (x >= xs_[b] && x < xe_[b]) ? 1.f : 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[k] += m * R.v[b][k];
     }
     float f[8];
     unpack8c(fv[t], f);
@@ -349,12 +475,14 @@ extern "C" int can_ctx_reduce(int mode, const void* in0, const void* sdir, const
                               int N, int h, int w, int C, void* stream) {
   if (C & 7) return -2;
   hipStream_t s = (hipStream_t)stream;
-  const size_t tr = (size_t)N * h * (C / 8);
+  if (w > 2048) return -3;                       // LDS bin-weight table [12][w]
+  const int nb = N * h * ((C / 8 + 63) / 64);
+  const size_t lds = (size_t)12 * w * sizeof(float);
   if (mode == 0)
-    hipLaunchKernelGGL(ctx_rows_kernel<true>, dim3(gridn(tr)), dim3(256), 0, s, (const uint4*)in0, nullptr, nullptr,
+    hipLaunchKernelGGL(ctx_rows_kernel<true>, dim3(nb), dim3(256), lds, s, (const uint4*)in0, nullptr, nullptr,
                        rowacc, N, h, w, C);
   else
-    hipLaunchKernelGGL(ctx_rows_kernel<false>, dim3(gridn(tr)), dim3(256), 0, s, nullptr, (const uint4*)sdir,
+    hipLaunchKernelGGL(ctx_rows_kernel<false>, dim3(nb), dim3(256), lds, s, nullptr, (const uint4*)sdir,
                        (const uint4*)dc, rowacc, N, h, w, C);
   const size_t tc = (size_t)N * 50 * C;
   if (mode == 0)
@@ -366,7 +494,7 @@ extern "C" int can_ctx_reduce(int mode, const void* in0, const void* sdir, const
 
 extern "C" int can_ctx_expand(const void* fv, const float* T, void* cs, int N, int h, int w, int C, void* stream) {
   if (C & 7) return -2;
-  hipLaunchKernelGGL(ctx_expand_kernel, dim3(gridn((size_t)N * h * w * (C / 8))), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(ctx_expand_kernel, dim3(N * h * ((C / 8 + 63) / 64) * 2), dim3(256), 0, (hipStream_t)stream,
                      (const uint4*)fv, T, (uint4*)cs, N, h, w, C);
   return (int)hipGetLastError();
 }
@@ -374,7 +502,7 @@ extern "C" int can_ctx_expand(const void* fv, const float* T, void* cs, int N, i
 extern "C" int can_ctx_fuse(const void* fv, const void* ws, const float* T, void* cat, int N, int h, int w, int C,
                             void* stream) {
   if (C & 7) return -2;
-  hipLaunchKernelGGL(ctx_fuse_kernel, dim3(gridn((size_t)N * h * w * (C / 8))), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(ctx_fuse_kernel, dim3(N * h * ((C / 8 + 63) / 64) * 2), dim3(256), 0, (hipStream_t)stream,
                      (const uint4*)fv, (const uint4*)ws, T, (uint4*)cat, N, h, w, C);
   return (int)hipGetLastError();
 }
@@ -382,7 +510,7 @@ extern "C" int can_ctx_fuse(const void* fv, const void* ws, const float* T, void
 extern "C" int can_ctx_bwd_e1(const void* dcat, const void* ws, const float* T, void* dz, void* sdir, int N, int h,
                               int w, int C, void* stream) {
   if (C & 7) return -2;
-  hipLaunchKernelGGL(ctx_bwd_e1_kernel, dim3(gridn((size_t)N * h * w * (C / 8))), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(ctx_bwd_e1_kernel, dim3(N * h * ((C / 8 + 63) / 64) * 2), dim3(256), 0, (hipStream_t)stream,
                      (const uint4*)dcat, (const uint4*)ws, T, (uint4*)dz, (uint4*)sdir, N, h, w, C);
   return (int)hipGetLastError();
 }
@@ -390,7 +518,7 @@ extern "C" int can_ctx_bwd_e1(const void* dcat, const void* ws, const float* T, 
 extern "C" int can_ctx_bwd_final(const void* dcat, const void* dc, const float* dave, const void* fv, void* dfv,
                                  int N, int h, int w, int C, void* stream) {
   if (C & 7) return -2;
-  hipLaunchKernelGGL(ctx_bwd_final_kernel, dim3(gridn((size_t)N * h * w * (C / 8))), dim3(256), 0,
+  hipLaunchKernelGGL(ctx_bwd_final_kernel, dim3(N * h * ((C / 8 + 63) / 64) * 2), dim3(256), 0,
                      (hipStream_t)stream, (const uint4*)dcat, (const uint4*)dc, dave, (const uint4*)fv, (uint4*)dfv, N,
                      h, w, C);
   return (int)hipGetLastError();
