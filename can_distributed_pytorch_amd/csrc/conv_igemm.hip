@@ -30,6 +30,7 @@
 //     sharing one pixel tile (and its halo) run on the same XCD / L2.
 #include "common.h"
 #include "fastdiv.h"
+#include <stdlib.h>
 
 namespace can {
 
@@ -794,6 +795,99 @@ __global__ void __launch_bounds__(512, 1) conv_halo64_kernel(HaloConvArgs a) {
   }
 }
 
+// ===========================================================================
+// First layer (conv1_1: 3 -> 64, 3x3, input NHWC4 bf16 = 8 B per pixel).
+// Output-write bound (805 MB of bf16 activations at batch 8 x 768 x 1024), so
+// the kernel does the minimum around the stores: the 6 x 130-pixel input halo
+// of a 4 x 128 output tile goes to LDS once (6.2 KB, plain 8-B loads); the
+// weights (packed [64][64], k = tap*4 + c) are MFMA A fragments loaded straight
+// into registers; each B fragment is two ds_read_b64 (taps 2q, 2q+1 of one
+// pixel, 4 channels each); K = 64 = 2 MFMA k-steps (taps 9..15 are zero).
+// ===========================================================================
+__global__ void __launch_bounds__(512) conv_first_halo_kernel(HaloConvArgs a) {
+  constexpr int TR = 4, TCOL = 128, HC = TCOL + 2, HPIX = (TR + 2) * HC;
+  __shared__ uint2 halo[HPIX];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ntile = a.N * a.tiles_y * a.tiles_x;
+  const int tile = xcd_remap(blockIdx.x, ntile);
+  const int tx = tile % a.tiles_x;
+  const int ty = (tile / a.tiles_x) % a.tiles_y;
+  const int n = tile / (a.tiles_x * a.tiles_y);
+  const int oh0 = ty * TR, ow0 = tx * TCOL;
+  const uint2* x8 = reinterpret_cast<const uint2*>(a.x);
+  for (int hp = tid; hp < HPIX; hp += 512) {
+    const int hr = hp / HC, hc = hp - hr * HC;
+    const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
+    uint2 v = make_uint2(0u, 0u);
+    if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) v = x8[(size_t)(n * a.H + ih) * a.W + iw];
+    halo[hp] = v;
+  }
+  const int fr = lane & 15, fq = lane >> 4;
+  bf16x8_t af[2][4];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      af[kk][j] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(a.w + perm_row(j * 16 + fr) * 64 + kk * 32 + fq * 8));
+  __syncthreads();
+
+  const int r = wave >> 1, colbase = (wave & 1) * 64;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int t0 = kk * 8 + fq * 2;                 // this lane's taps t0, t0+1
+    bf16x8_t bfr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      uint2 lo = make_uint2(0u, 0u), hi = make_uint2(0u, 0u);
+      const int c = colbase + i * 16 + fr;
+      if (t0 < 9) {
+        const int kh = (t0 * 11) >> 5, kw = t0 - kh * 3;
+        lo = halo[(r + kh) * HC + c + kw];
+      }
+      if (t0 + 1 < 9) {
+        const int kh = ((t0 + 1) * 11) >> 5, kw = t0 + 1 - kh * 3;
+        hi = halo[(r + kh) * HC + c + kw];
+      }
+      bfr[i] = __builtin_bit_cast(bf16x8_t, make_uint4(lo.x, lo.y, hi.x, hi.y));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][j], bfr[i], acc[j][i], 0, 0, 0);
+  }
+
+  const int oh = oh0 + r;
+  if (oh >= a.H) return;
+  const int chb = fq * 16;
+  float bias[16];
+#pragma unroll
+  for (int c = 0; c < 16; c += 4) {
+    const float4 b4 = *reinterpret_cast<const float4*>(a.bias + chb + c);
+    bias[c] = b4.x; bias[c + 1] = b4.y; bias[c + 2] = b4.z; bias[c + 3] = b4.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int ow = ow0 + colbase + i * 16 + fr;
+    if (ow >= a.W) continue;
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[j * 4 + q] = fmaxf(acc[j][i][q] + bias[j * 4 + q], 0.f);
+    const size_t off = ((size_t)(n * a.H + oh) * a.W + ow) * 64 + chb;
+    *reinterpret_cast<uint4*>(a.y + off) =
+        make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
+    *reinterpret_cast<uint4*>(a.y + off + 8) =
+        make_uint4(pack2bf(v[8], v[9]), pack2bf(v[10], v[11]), pack2bf(v[12], v[13]), pack2bf(v[14], v[15]));
+  }
+}
+
 template <int CO, int EPI>
 static int launch_halo64(const HaloConvArgs& a, hipStream_t s) {
   constexpr int HALO_BYTES = ((6 * 130 + 7) / 8) * 1024;
@@ -863,10 +957,20 @@ extern "C" int can_conv_igemm(const void* x, const void* w, const float* bias, c
   hipStream_t s = (hipStream_t)stream;
 #define CAN_EPI_CASE(L, E) \
   if (epi == E) return dispatch_tiles<L, E>(a, tile_cfg, s);
+  const bool auto_halo = tile_cfg == 0 && getenv("CANNET_NO_HALO_CONV") == nullptr;
   if (first) {
+    if ((tile_cfg == 32 || auto_halo) && Cout == 64 && epi == EPI_BIAS_RELU) {
+      HaloConvArgs h;
+      h.x = a.x; h.w = a.w; h.bias = a.bias; h.mask = nullptr; h.y = a.y; h.zero = nullptr;
+      h.N = N; h.H = H; h.W = W; h.tiles_x = (W + 127) / 128; h.tiles_y = (H + 3) / 4;
+      hipLaunchKernelGGL(conv_first_halo_kernel, dim3(N * h.tiles_y * h.tiles_x), dim3(512), 0, s, h);
+      return (int)hipGetLastError();
+    }
     CAN_EPI_CASE(LOAD_FIRST, EPI_BIAS_RELU)
     return -5;
   }
+  if (auto_halo && Cin == 64 && ksize == 3 && dil == 1 && (Cout == 64 || Cout == 128) && epi != EPI_SIGMOID)
+    tile_cfg = 31;
   if (tile_cfg == 31) {
     // halo-tiled Cin = 64 kernel (explicit; see conv_halo64_kernel)
     if (Cin != 64 || ksize != 3 || dil != 1 || (Cout != 64 && Cout != 128)) return -11;

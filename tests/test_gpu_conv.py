@@ -48,14 +48,16 @@ def test_conv_fwd(n, h, w, ci, co, k, dil, tile):
     _close(y, _ref(x, wt, b, dil))
 
 
-def test_conv_first_layer():
+@pytest.mark.parametrize("n,h,w,tile", [(2, 40, 56, 0), (1, 37, 150, 0), (2, 8, 256, 0), (2, 40, 56, 1)])
+def test_conv_first_layer(n, h, w, tile):
+    """tile 0: halo-tiled first-layer kernel; tile 1: register-staged generic kernel."""
     from can_distributed_pytorch_amd.ops import conv as C
     torch.manual_seed(1)
-    img = torch.randn(2, 3, 40, 56, device="cuda")
+    img = torch.randn(n, 3, h, w, device="cuda")
     wt = (torch.randn(64, 3, 3, 3, device="cuda") * 0.2).to(torch.bfloat16).float()
     b = torch.randn(64, device="cuda")
     x4 = C.to_nhwc4(img)
-    y = C.conv_igemm(x4, C.pack_weight_first(wt), b, ksize=3, first=True)
+    y = C.conv_igemm(x4, C.pack_weight_first(wt), b, ksize=3, first=True, tile=tile)
     ref = _ref(x4[..., :3].contiguous(), wt, b, 1)
     _close(y, ref)
 
