@@ -567,58 +567,7 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
 
   const int nco = a.Cout / TCo, nkt = a.K / TK;
   const int ntile = nco * nkt;
-  const int nbias = (a.wsb != nullptr) ? a.S : 0;
-
-  // ---- bias blocks (first in the grid, so they overlap the GEMM blocks):
-  // db partial of one pixel slice = column sums of dY, plain loads + VALU
-  if ((int)blockIdx.x < nbias) {
-    const int slice = blockIdx.x;
-    const int mbeg = slice * a.mslice, mend = min(a.M, mbeg + a.mslice);
-    const int cg = tid & 63, rg = tid >> 6;      // 8-channel group, row group (NW row groups)
-    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (cg * 8 < a.Cout) {
-      const bf16_t* base = a.dy + cg * 8;
-      int m = mbeg + rg;
-      for (; m + 3 * NW < mend; m += 4 * NW) {
-        uint4 v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const uint4*>(base + (size_t)(m + u * NW) * a.Cout);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const unsigned w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-          for (int e2 = 0; e2 < 4; ++e2) {
-            s[2 * e2] += __uint_as_float(w4[e2] << 16);
-            s[2 * e2 + 1] += __uint_as_float(w4[e2] & 0xffff0000u);
-          }
-        }
-      }
-      for (; m < mend; m += NW) {
-        const uint4 v = *reinterpret_cast<const uint4*>(base + (size_t)m * a.Cout);
-        const unsigned w4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int e2 = 0; e2 < 4; ++e2) {
-          s[2 * e2] += __uint_as_float(w4[e2] << 16);
-          s[2 * e2 + 1] += __uint_as_float(w4[e2] & 0xffff0000u);
-        }
-      }
-    }
-    float* red = reinterpret_cast<float*>(smem);   // [NW][64][8]
-#pragma unroll
-    for (int e2 = 0; e2 < 8; ++e2) red[(rg * 64 + cg) * 8 + e2] = s[e2];
-    __syncthreads();
-    if (rg == 0 && cg * 8 < a.Cout) {
-#pragma unroll
-      for (int e2 = 0; e2 < 8; ++e2) {
-        float t = 0.f;
-        for (int r = 0; r < NW; ++r) t += red[(r * 64 + cg) * 8 + e2];
-        a.wsb[(size_t)slice * a.Cout + cg * 8 + e2] = t;
-      }
-    }
-    return;
-  }
-
-  const int bid = xcd_remap(blockIdx.x - nbias, ntile * a.S);
+  const int bid = xcd_remap(blockIdx.x, ntile * a.S);
   const int tile = bid % ntile, slice = bid / ntile;
   const int co0 = (tile % nco) * TCo, k0 = (tile / nco) * TK;
   const int mbeg = slice * a.mslice;
@@ -759,6 +708,58 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
     }
 }
 
+// Bias gradient partials for the v2 path: part[b][co] = sum of dY rows of
+// chunk b (SB chunks, fixed order; wgrad_reduce sums the SB partials).  A
+// separate short launch with many blocks, so the GEMM grid stays whole rounds.
+__global__ void __launch_bounds__(256) bias_colsum_kernel(const bf16_t* __restrict__ dy, float* __restrict__ part,
+                                                          int M, int Cout, int SB) {
+  __shared__ float red[256 * 8];
+  const int C8 = Cout >> 3;
+  const int groups = 256 / C8;                    // row groups (C8 <= 256 -> >= 1)
+  const int cg = threadIdx.x % C8, rg = threadIdx.x / C8;
+  const int rows = (M + SB - 1) / SB;
+  const int m0 = blockIdx.x * rows, m1 = min(M, m0 + rows);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (rg < groups) {
+    const bf16_t* base = dy + cg * 8;
+    int m = m0 + rg;
+    for (; m + 3 * groups < m1; m += 4 * groups) {
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const uint4*>(base + (size_t)(m + u * groups) * Cout);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const unsigned w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+        for (int e2 = 0; e2 < 4; ++e2) {
+          s[2 * e2] += __uint_as_float(w4[e2] << 16);
+          s[2 * e2 + 1] += __uint_as_float(w4[e2] & 0xffff0000u);
+        }
+      }
+    }
+    for (; m < m1; m += groups) {
+      const uint4 v = *reinterpret_cast<const uint4*>(base + (size_t)m * Cout);
+      const unsigned w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e2 = 0; e2 < 4; ++e2) {
+        s[2 * e2] += __uint_as_float(w4[e2] << 16);
+        s[2 * e2 + 1] += __uint_as_float(w4[e2] & 0xffff0000u);
+      }
+    }
+  }
+#pragma unroll
+  for (int e2 = 0; e2 < 8; ++e2) red[threadIdx.x * 8 + e2] = s[e2];
+  __syncthreads();
+  if (rg == 0) {
+#pragma unroll
+    for (int e2 = 0; e2 < 8; ++e2) {
+      float t = 0.f;
+      for (int r = 0; r < groups; ++r) t += red[(r * C8 + cg) * 8 + e2];
+      part[(size_t)blockIdx.x * Cout + cg * 8 + e2] = t;
+    }
+  }
+}
+
 template <int WC, int WK, int KW>
 static int launch_wgrad3(const WgradArgs2& a, hipStream_t s) {
   constexpr int STAGE = 64 * (64 * WC + 64 * WK * KW) * 2;
@@ -770,8 +771,7 @@ static int launch_wgrad3(const WgradArgs2& a, hipStream_t s) {
     attr = true;
   }
   const int ntile = (a.Cout / (64 * WC)) * (a.K / (64 * WK * KW));
-  const int nbias = (a.wsb != nullptr) ? a.S : 0;
-  hipLaunchKernelGGL(kfn, dim3(nbias + ntile * a.S), dim3(64 * WC * WK), lds, s, a);
+  hipLaunchKernelGGL(kfn, dim3(ntile * a.S), dim3(64 * WC * WK), lds, s, a);
   return (int)hipGetLastError();
 }
 
@@ -953,7 +953,7 @@ static int launch_halo(HaloArgs& a, hipStream_t s) {
 // deterministic, and enough loads in flight for S in the hundreds.
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ ws, const float* __restrict__ wsb,
                                                            float* __restrict__ dw, float* __restrict__ db, int S,
-                                                           int Ktot, int Cout, int Cin, int taps, int first,
+                                                           int Sb, int Ktot, int Cout, int Cin, int taps, int first,
                                                            float beta, float scale) {
   __shared__ float part[4][64];
   const int e = threadIdx.x & 63, grp = threadIdx.x >> 6;
@@ -977,7 +977,7 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
       const int c = c0 + e;
       float t = 0.f;
       if (c < Cout)
-        for (int sl = grp; sl < S; sl += 4) t += wsb[(size_t)sl * Cout + c];
+        for (int sl = grp; sl < Sb; sl += 4) t += wsb[(size_t)sl * Cout + c];
       part[grp][e] = t;
       __syncthreads();
       if (grp == 0 && c < Cout) {
@@ -1031,6 +1031,9 @@ static int launch_wgrad(const WgradArgs& a, hipStream_t s) {
 // 2 = 256co x 128k (8 waves, 3 bufs), 3 = 64co x 128k (4 waves, pixel-split 2,
 // 3 bufs), 4 = 64co x 64k (2 waves, pixel-split 2, 4 bufs); 0 = first layer
 // (register-staged kernel).
+// bias partial count of the v2 path (workspace: max(S, kBiasParts) x Cout floats)
+static constexpr int kBiasParts = 128;
+
 static void wgrad_tile(int cfg, int* TCo, int* TK, int* BKM) {
   switch (cfg) {
     case 1: *TCo = 128; *TK = 128; *BKM = 64; break;
@@ -1119,6 +1122,7 @@ extern "C" int can_conv_wgrad(const void* dy, const void* x, float* ws, float* w
   const int K = first ? 64 : ksize * ksize * Cin;
   float* wsb_used = (db != nullptr) ? wsb : nullptr;
   int rc;
+  int Sb = S;                       // bias partials summed by the reduce kernel
   if (first || cfg == 0) {
     if (Cin != 4 || Cout % 64) return -2;
     WgradArgs a;
@@ -1145,7 +1149,7 @@ extern "C" int can_conv_wgrad(const void* dy, const void* x, float* ws, float* w
       if (rc) return rc;
       const int plane = K * Cout;
       hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((plane + 63) / 64 + 1), dim3(256), 0, s, ws, wsb_used, dw, db, S,
-                         K, Cout, Cin, 9, 0, beta, scale);
+                         S, K, Cout, Cin, 9, 0, beta, scale);
       return (int)hipGetLastError();
     }
     switch (cfg) {
@@ -1158,9 +1162,16 @@ extern "C" int can_conv_wgrad(const void* dy, const void* x, float* ws, float* w
       case 7: if (Cout % 256) return -4; rc = launch_wgrad2<4, 2, 1, 2, 2, 2>(a, s); break;
       case 9:
         if (Cout % 256) return -4;
-        if (W % 64 == 0 && Cin % 256 == 0 && mslice % 64 == 0 && (long long)a.M * Cout * 2 < 0x7fffffffLL)
-          rc = launch_wgrad3<4, 2, 2>(a, s);
-        else
+        if (W % 64 == 0 && Cin % 256 == 0 && mslice % 64 == 0 && (long long)a.M * Cout * 2 < 0x7fffffffLL &&
+            Cout <= 2048) {
+          if (wsb_used) {
+            Sb = kBiasParts;
+            hipLaunchKernelGGL(bias_colsum_kernel, dim3(Sb), dim3(256), 0, s, a.dy, wsb_used, a.M, Cout, Sb);
+          }
+          WgradArgs2 g = a;
+          g.wsb = nullptr;
+          rc = launch_wgrad3<4, 2, 2>(g, s);
+        } else
           rc = launch_wgrad2<4, 2, 1, 2, 2, 2>(a, s);   // same tiles / slicing as cfg 7
         break;
       default: return -5;
@@ -1168,7 +1179,7 @@ extern "C" int can_conv_wgrad(const void* dy, const void* x, float* ws, float* w
   }
   if (rc) return rc;
   const int plane = K * Cout;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((plane + 63) / 64 + 1), dim3(256), 0, s, ws, wsb_used, dw, db, S, K,
-                     Cout, first ? 4 : Cin, ksize * ksize, first, beta, scale);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((plane + 63) / 64 + 1), dim3(256), 0, s, ws, wsb_used, dw, db, S, Sb,
+                     K, Cout, first ? 4 : Cin, ksize * ksize, first, beta, scale);
   return (int)hipGetLastError();
 }
