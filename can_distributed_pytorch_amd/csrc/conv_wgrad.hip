@@ -945,68 +945,6 @@ static int launch_halo(HaloArgs& a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-// Sum S slabs [S][K][Cout] in a fixed order and write dW in the PyTorch layout
-// [Cout][Cin][kh][kw] (first layer: Cin = 3 real channels of the k = tap*4 + c
-// packing).  beta = 0 overwrites, 1 accumulates.  Block = 64 consecutive
-// elements x 4 slice groups (each thread sums a strided quarter of the slices
-// with 4 independent accumulators), combined in LDS in a fixed order:
-// deterministic, and enough loads in flight for S in the hundreds.
-__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ ws, const float* __restrict__ wsb,
-                                                           float* __restrict__ dw, float* __restrict__ db, int S,
-                                                           int Sb, int Ktot, int Cout, int Cin, int taps, int first,
-                                                           float beta, float scale) {
-  __shared__ float part[4][64];
-  const int e = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const size_t plane = (size_t)Ktot * Cout;
-  const size_t idx = (size_t)blockIdx.x * 64 + e;
-  const bool is_bias = blockIdx.x == gridDim.x - 1;      // last block: bias
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  if (!is_bias) {
-    if (idx < plane) {
-      int sl = grp;
-      for (; sl + 12 < S; sl += 16) {
-        s0 += ws[(size_t)sl * plane + idx];
-        s1 += ws[(size_t)(sl + 4) * plane + idx];
-        s2 += ws[(size_t)(sl + 8) * plane + idx];
-        s3 += ws[(size_t)(sl + 12) * plane + idx];
-      }
-      for (; sl < S; sl += 4) s0 += ws[(size_t)sl * plane + idx];
-    }
-  } else if (db != nullptr) {
-    for (int c0 = 0; c0 < Cout; c0 += 64) {
-      const int c = c0 + e;
-      float t = 0.f;
-      if (c < Cout)
-        for (int sl = grp; sl < Sb; sl += 4) t += wsb[(size_t)sl * Cout + c];
-      part[grp][e] = t;
-      __syncthreads();
-      if (grp == 0 && c < Cout) {
-        const float v = (part[0][e] + part[1][e] + part[2][e] + part[3][e]) * scale;
-        db[c] = (beta != 0.f) ? db[c] * beta + v : v;
-      }
-      __syncthreads();
-    }
-    return;
-  } else {
-    return;
-  }
-  part[grp][e] = (s0 + s1) + (s2 + s3);
-  __syncthreads();
-  if (grp == 0 && idx < plane) {
-    const float v = (part[0][e] + part[1][e] + part[2][e] + part[3][e]) * scale;
-    const int co = idx % Cout, k = idx / Cout;
-    int ci, tap;
-    bool valid = true;
-    if (first) { tap = k >> 2; ci = k & 3; valid = (tap < 9) && (ci < 3); }
-    else { tap = k / Cin; ci = k - tap * Cin; }
-    if (valid) {
-      const int cin_t = first ? 3 : Cin;
-      float* o = dw + ((size_t)co * cin_t + ci) * taps + tap;
-      *o = (beta != 0.f) ? (*o * beta + v) : v;
-    }
-  }
-}
-
 template <int WC, int WK, int WM, bool FIRST>
 static int launch_wgrad(const WgradArgs& a, hipStream_t s) {
   constexpr int TCo = 64 * WC, TK = 64 * WK;
@@ -1031,8 +969,102 @@ static int launch_wgrad(const WgradArgs& a, hipStream_t s) {
 // 2 = 256co x 128k (8 waves, 3 bufs), 3 = 64co x 128k (4 waves, pixel-split 2,
 // 3 bufs), 4 = 64co x 64k (2 waves, pixel-split 2, 4 bufs); 0 = first layer
 // (register-staged kernel).
+namespace can {
+// Sum S slabs [S][K][Cout] in a fixed order and write dW in the PyTorch layout
+// [Cout][Cin][kh][kw] (first layer: Cin = 3 real channels of the k = tap*4 + c
+// packing); beta = 0 overwrites, 1 accumulates.
+// Grid-stride slab reduction (v2): SG slice groups x (256/SG) elements per
+// block, grid capped at 4096 blocks (the element-per-block form was bound by
+// block dispatch for S ~ 7 and planes of millions of elements).  Each group
+// sums slices sl = g, g+SG, ... in order with 4 accumulators; groups combine in
+// LDS in a fixed order: deterministic.  The last block reduces the bias parts.
+template <int SG>
+__global__ void __launch_bounds__(256) wgrad_reduce2_kernel(const float* __restrict__ ws, const float* __restrict__ wsb,
+                                                            float* __restrict__ dw, float* __restrict__ db, int S,
+                                                            int Sb, int Ktot, int Cout, int Cin, int taps, int first,
+                                                            float beta, float scale) {
+  constexpr int EPB = 256 / SG;
+  __shared__ float part[SG][EPB];
+  __shared__ float bpart[4][64];
+  const int e = threadIdx.x % EPB, grp = threadIdx.x / EPB;
+  const size_t plane = (size_t)Ktot * Cout;
+  if (blockIdx.x == gridDim.x - 1) {
+    if (db == nullptr) return;
+    const int e64 = threadIdx.x & 63, g4 = threadIdx.x >> 6;
+    for (int c0 = 0; c0 < Cout; c0 += 64) {
+      const int c = c0 + e64;
+      float t = 0.f;
+      if (c < Cout)
+        for (int sl = g4; sl < Sb; sl += 4) t += wsb[(size_t)sl * Cout + c];
+      bpart[g4][e64] = t;
+      __syncthreads();
+      if (g4 == 0 && c < Cout) {
+        const float v = (bpart[0][e64] + bpart[1][e64] + bpart[2][e64] + bpart[3][e64]) * scale;
+        db[c] = (beta != 0.f) ? db[c] * beta + v : v;
+      }
+      __syncthreads();
+    }
+    return;
+  }
+  const int cin_t = first ? 3 : Cin;
+  for (size_t base = (size_t)blockIdx.x * EPB; base < plane; base += (size_t)(gridDim.x - 1) * EPB) {
+    const size_t idx = base + e;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    if (idx < plane) {
+      int sl = grp;
+      for (; sl + 3 * SG < S; sl += 4 * SG) {
+        s0 += ws[(size_t)sl * plane + idx];
+        s1 += ws[(size_t)(sl + SG) * plane + idx];
+        s2 += ws[(size_t)(sl + 2 * SG) * plane + idx];
+        s3 += ws[(size_t)(sl + 3 * SG) * plane + idx];
+      }
+      for (; sl < S; sl += SG) s0 += ws[(size_t)sl * plane + idx];
+    }
+    float v = (s0 + s1) + (s2 + s3);
+    if (SG > 1) {
+      part[grp][e] = v;
+      __syncthreads();
+      v = 0.f;
+      if (grp == 0)
+#pragma unroll
+        for (int g = 0; g < SG; ++g) v += part[g][e];
+      __syncthreads();
+    }
+    if (grp == 0 && idx < plane) {
+      v *= scale;
+      const int co = (int)(idx % Cout), k = (int)(idx / Cout);
+      int ci, tap;
+      bool valid = true;
+      if (first) { tap = k >> 2; ci = k & 3; valid = (tap < 9) && (ci < 3); }
+      else { tap = k / Cin; ci = k - tap * Cin; }
+      if (valid) {
+        float* o = dw + ((size_t)co * cin_t + ci) * taps + tap;
+        *o = (beta != 0.f) ? (*o * beta + v) : v;
+      }
+    }
+  }
+}
+
+static int launch_reduce2(const float* ws, const float* wsb, float* dw, float* db, int S, int Sb, int K, int Cout,
+                          int Cin, int taps, int first, float beta, float scale, hipStream_t s) {
+  const size_t plane = (size_t)K * Cout;
+  auto grid = [&](int epb) { return (int)std::min<size_t>((plane + epb - 1) / epb, 4096) + 1; };
+  if (S <= 16)
+    hipLaunchKernelGGL(wgrad_reduce2_kernel<1>, dim3(grid(256)), dim3(256), 0, s, ws, wsb, dw, db, S, Sb, K, Cout,
+                       Cin, taps, first, beta, scale);
+  else if (S <= 128)
+    hipLaunchKernelGGL(wgrad_reduce2_kernel<4>, dim3(grid(64)), dim3(256), 0, s, ws, wsb, dw, db, S, Sb, K, Cout,
+                       Cin, taps, first, beta, scale);
+  else
+    hipLaunchKernelGGL(wgrad_reduce2_kernel<16>, dim3(grid(16)), dim3(256), 0, s, ws, wsb, dw, db, S, Sb, K, Cout,
+                       Cin, taps, first, beta, scale);
+  return (int)hipGetLastError();
+}
+}  // namespace can
+using namespace can;
+
 // bias partial count of the v2 path (workspace: max(S, kBiasParts) x Cout floats)
-static constexpr int kBiasParts = 128;
+static constexpr int kBiasParts = 512;
 
 static void wgrad_tile(int cfg, int* TCo, int* TK, int* BKM) {
   switch (cfg) {
@@ -1148,9 +1180,7 @@ extern "C" int can_conv_wgrad(const void* dy, const void* x, float* ws, float* w
       rc = launch_halo<64, 2>(h, s);   // Cout = 128 runs as two 64-channel co tiles
       if (rc) return rc;
       const int plane = K * Cout;
-      hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((plane + 63) / 64 + 1), dim3(256), 0, s, ws, wsb_used, dw, db, S,
-                         S, K, Cout, Cin, 9, 0, beta, scale);
-      return (int)hipGetLastError();
+      return launch_reduce2(ws, wsb_used, dw, db, S, S, K, Cout, Cin, 9, 0, beta, scale, s);
     }
     switch (cfg) {
       case 1: if (Cout % 128) return -4; rc = launch_wgrad2<2, 2, 1, 4, 1, 2>(a, s); break;
@@ -1179,7 +1209,6 @@ extern "C" int can_conv_wgrad(const void* dy, const void* x, float* ws, float* w
   }
   if (rc) return rc;
   const int plane = K * Cout;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((plane + 63) / 64 + 1), dim3(256), 0, s, ws, wsb_used, dw, db, S, Sb,
-                     K, Cout, first ? 4 : Cin, ksize * ksize, first, beta, scale);
-  return (int)hipGetLastError();
+  (void)plane;
+  return launch_reduce2(ws, wsb_used, dw, db, S, Sb, K, Cout, first ? 4 : Cin, ksize * ksize, first, beta, scale, s);
 }

@@ -118,7 +118,7 @@ class WgradWorkspace:
         C = _ext.require()
         s, mslice, cfg = C.wgrad_plan(m, ci, co, ksize, int(first), self.target_blocks)
         ktot = 64 if first else ksize * ksize * ci
-        need = s * ktot * co + max(s, 128) * co      # slabs + bias partials (v2 path: 128 column-sum parts)
+        need = s * ktot * co + max(s, 512) * co      # slabs + bias partials (v2 path: 512 column-sum parts)
         return s, mslice, cfg, need
 
     def reserve(self, need: int) -> torch.Tensor:
