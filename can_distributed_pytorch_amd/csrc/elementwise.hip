@@ -159,14 +159,31 @@ __global__ void __launch_bounds__(256) head_train_kernel(const uint4* __restrict
   }
 }
 
-// out[0..63] = dw, out[64] = db, loss_out[0] = loss  (fixed-order, deterministic)
-__global__ void __launch_bounds__(128) head_reduce_kernel(const float* __restrict__ part, int nblk,
-                                                          float* __restrict__ dw, float* __restrict__ db,
-                                                          float* __restrict__ loss, float beta) {
+// out[0..63] = dw, out[64] = db, loss_out[0] = loss  (fixed-order, deterministic):
+// 15 groups x 66 outputs, group g sums blocks g, g+15, ... then the 15 group
+// sums are added in order (a single thread per output serialised ~1k loads).
+__global__ void __launch_bounds__(1024) head_reduce_kernel(const float* __restrict__ part, int nblk,
+                                                           float* __restrict__ dw, float* __restrict__ db,
+                                                           float* __restrict__ loss, float beta) {
+  constexpr int G = 15;
+  __shared__ float red[G][66];
   const int t = threadIdx.x;
+  const int o = t % 66, g = t / 66;
+  if (g < G) {
+    float s0 = 0.f, s1 = 0.f;
+    int i = g;
+    for (; i + G < nblk; i += 2 * G) {
+      s0 += part[(size_t)i * 66 + o];
+      s1 += part[(size_t)(i + G) * 66 + o];
+    }
+    if (i < nblk) s0 += part[(size_t)i * 66 + o];
+    red[g][o] = s0 + s1;
+  }
+  __syncthreads();
   if (t < 66) {
     float s = 0.f;
-    for (int i = 0; i < nblk; ++i) s += part[(size_t)i * 66 + t];
+#pragma unroll
+    for (int q = 0; q < G; ++q) s += red[q][t];
     if (t < 64) dw[t] = (beta != 0.f) ? dw[t] * beta + s : s;
     else if (t == 64) db[0] = (beta != 0.f) ? db[0] * beta + s : s;
     else loss[0] = s;
@@ -274,7 +291,7 @@ extern "C" int can_head_train(const void* y, const float* w, const float* b, con
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(head_train_kernel, dim3(nblk), dim3(256), 0, s, (const uint4*)y, w, b, gt, et, (uint4*)dy, part,
                      P, gscale);
-  hipLaunchKernelGGL(head_reduce_kernel, dim3(1), dim3(128), 0, s, part, nblk, dw, db, loss, beta);
+  hipLaunchKernelGGL(head_reduce_kernel, dim3(1), dim3(1024), 0, s, part, nblk, dw, db, loss, beta);
   return (int)hipGetLastError();
 }
 
