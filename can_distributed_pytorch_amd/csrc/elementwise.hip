@@ -239,6 +239,30 @@ __global__ void __launch_bounds__(256) pack_conv_kernel(const float* __restrict_
   }
 }
 
+// All layers' packs in one launch: blockIdx.y = layer, descriptor rows
+// {w, fwd, dgr, Co, Ci, taps, first, 0} (int64), blocks grid-stride in a layer.
+__global__ void __launch_bounds__(256) pack_multi_kernel(const long long* __restrict__ desc) {
+  const long long* d = desc + (size_t)blockIdx.y * 8;
+  const float* w = reinterpret_cast<const float*>(d[0]);
+  bf16_t* fwd = reinterpret_cast<bf16_t*>(d[1]);
+  bf16_t* dgr = reinterpret_cast<bf16_t*>(d[2]);
+  const int Co = (int)d[3], Ci = (int)d[4], taps = (int)d[5], first = (int)d[6];
+  const size_t total = (size_t)Co * Ci * taps;
+  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const int tap = i % taps;
+    const size_t r = i / taps;
+    const int ci = r % Ci;
+    const int co = r / Ci;
+    const unsigned short v = f2bf(w[i]);
+    if (first) {
+      fwd[(size_t)co * 64 + tap * 4 + ci] = v;
+    } else {
+      fwd[((size_t)co * taps + tap) * Ci + ci] = v;
+      if (dgr) dgr[((size_t)ci * taps + (taps - 1 - tap)) * Co + co] = v;
+    }
+  }
+}
+
 // [N,3,H,W] fp32 -> [N,H,W,4] bf16 (4th channel zero)
 __global__ void __launch_bounds__(256) img_to_nhwc4_kernel(const float* __restrict__ img, uint2* __restrict__ out,
                                                            int N, int H, int W) {
@@ -313,5 +337,11 @@ extern "C" int can_pack_conv(const float* w, void* fwd, void* dgr, int Co, int C
 extern "C" int can_img_to_nhwc4(const float* img, void* out, int N, int H, int W, void* stream) {
   hipLaunchKernelGGL(img_to_nhwc4_kernel, dim3(grid_for((size_t)N * H * W, 256, 8192)), dim3(256), 0,
                      (hipStream_t)stream, img, (uint2*)out, N, H, W);
+  return (int)hipGetLastError();
+}
+
+extern "C" int can_pack_multi(const long long* desc, int layers, void* stream) {
+  if (layers <= 0) return 0;
+  hipLaunchKernelGGL(pack_multi_kernel, dim3(96, layers), dim3(256), 0, (hipStream_t)stream, desc);
   return (int)hipGetLastError();
 }

@@ -82,6 +82,8 @@ class CANNetExecutor:
         self.ctx2_index = {s: pid[id(self.ctx2[s].weight)] for s in CONTEXT_SCALES}
         self.packs: Dict[int, tuple] = {}
         self._pack_version = None
+        self._pack_desc = None          # device descriptor rows of the batched pack launch
+        self._pack_desc_ptrs = None
         self.ws = None
         self.stream_override = None
 
@@ -120,7 +122,7 @@ class CANNetExecutor:
                                  torch.empty(512, 512, dtype=BF16, device=device))
 
     def refresh_packs(self, force: bool = False):
-        """Re-pack bf16 weight copies from the fp32 masters (one kernel per layer)."""
+        """Re-pack bf16 weight copies from the fp32 masters (one launch for all layers)."""
         ver = self._weights_version()
         if not force and ver == self._pack_version and self.packs:
             return
@@ -128,15 +130,25 @@ class CANNetExecutor:
         if not self.packs:
             self._alloc_packs(dev)
         st = self._stream()
-        for s in self.front + self.back:
-            w = s.module.weight.detach()
-            fwd, dgr = self.packs[id(s.module.weight)]
-            self.C.pack_conv(w.data_ptr(), fwd.data_ptr(), dgr.data_ptr() if dgr is not None else 0, s.cout, s.cin,
-                             s.ksize * s.ksize, int(s.first), st)
-        for sc in CONTEXT_SCALES:
-            w = self.ctx2[sc].weight.detach()
-            fwd, dgr = self.packs[id(self.ctx2[sc].weight)]
-            self.C.pack_conv(w.data_ptr(), fwd.data_ptr(), dgr.data_ptr(), 512, 512, 1, 0, st)
+        if self._pack_desc is None:
+            rows = []
+            for s in self.front + self.back:
+                fwd, dgr = self.packs[id(s.module.weight)]
+                rows.append([s.module.weight.data_ptr(), fwd.data_ptr(), dgr.data_ptr() if dgr is not None else 0,
+                             s.cout, s.cin, s.ksize * s.ksize, int(s.first), 0])
+            for sc in CONTEXT_SCALES:
+                fwd, dgr = self.packs[id(self.ctx2[sc].weight)]
+                rows.append([self.ctx2[sc].weight.data_ptr(), fwd.data_ptr(), dgr.data_ptr(), 512, 512, 1, 0, 0])
+            self._pack_desc = torch.tensor(rows, dtype=torch.int64, device=dev)
+            self._pack_desc_ptrs = tuple(r[0] for r in rows)
+        # one launch for every layer (descriptor rows hold the fp32 master pointers,
+        # which the flat arena keeps fixed; rebuilt if a weight tensor moved)
+        cur = tuple(s.module.weight.data_ptr() for s in self.front + self.back) + \
+            tuple(self.ctx2[sc].weight.data_ptr() for sc in CONTEXT_SCALES)
+        if cur != self._pack_desc_ptrs:
+            self._pack_desc = None
+            return self.refresh_packs(force=True)
+        self.C.pack_multi(self._pack_desc.data_ptr(), self._pack_desc.shape[0], st)
         self._pack_version = ver
 
     def mark_weights_updated(self):
