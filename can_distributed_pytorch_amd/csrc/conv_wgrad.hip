@@ -977,7 +977,7 @@ namespace can {
 // block, grid capped at 4096 blocks (the element-per-block form was bound by
 // block dispatch for S ~ 7 and planes of millions of elements).  Each group
 // sums slices sl = g, g+SG, ... in order with 4 accumulators; groups combine in
-// LDS in a fixed order: deterministic.  The last block reduces the bias parts.
+// LDS in a fixed order: deterministic.  The last Cout/16 blocks reduce the bias parts.
 template <int SG>
 __global__ void __launch_bounds__(256) wgrad_reduce2_kernel(const float* __restrict__ ws, const float* __restrict__ wsb,
                                                             float* __restrict__ dw, float* __restrict__ db, int S,
@@ -985,29 +985,36 @@ __global__ void __launch_bounds__(256) wgrad_reduce2_kernel(const float* __restr
                                                             float beta, float scale) {
   constexpr int EPB = 256 / SG;
   __shared__ float part[SG][EPB];
-  __shared__ float bpart[4][64];
+  __shared__ float bpart[16][16];
   const int e = threadIdx.x % EPB, grp = threadIdx.x / EPB;
   const size_t plane = (size_t)Ktot * Cout;
-  if (blockIdx.x == gridDim.x - 1) {
-    if (db == nullptr) return;
-    const int e64 = threadIdx.x & 63, g4 = threadIdx.x >> 6;
-    for (int c0 = 0; c0 < Cout; c0 += 64) {
-      const int c = c0 + e64;
-      float t = 0.f;
-      if (c < Cout)
-        for (int sl = g4; sl < Sb; sl += 4) t += wsb[(size_t)sl * Cout + c];
-      bpart[g4][e64] = t;
-      __syncthreads();
-      if (g4 == 0 && c < Cout) {
-        const float v = (bpart[0][e64] + bpart[1][e64] + bpart[2][e64] + bpart[3][e64]) * scale;
-        db[c] = (beta != 0.f) ? db[c] * beta + v : v;
+  const int nbias = (db != nullptr) ? (Cout + 15) / 16 : 0;
+  const int nmain = gridDim.x - nbias;
+  if ((int)blockIdx.x >= nmain) {
+    // bias: block = 16 channels x 16 part groups (group g sums parts g, g+16, ...)
+    const int c = ((int)blockIdx.x - nmain) * 16 + (threadIdx.x & 15), g = threadIdx.x >> 4;
+    float t0 = 0.f, t1 = 0.f;
+    if (c < Cout) {
+      int sl = g;
+      for (; sl + 16 < Sb; sl += 32) {
+        t0 += wsb[(size_t)sl * Cout + c];
+        t1 += wsb[(size_t)(sl + 16) * Cout + c];
       }
-      __syncthreads();
+      if (sl < Sb) t0 += wsb[(size_t)sl * Cout + c];
+    }
+    bpart[g][threadIdx.x & 15] = t0 + t1;
+    __syncthreads();
+    if (g == 0 && c < Cout) {
+      float v = 0.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v += bpart[q][threadIdx.x & 15];
+      v *= scale;
+      db[c] = (beta != 0.f) ? db[c] * beta + v : v;
     }
     return;
   }
   const int cin_t = first ? 3 : Cin;
-  for (size_t base = (size_t)blockIdx.x * EPB; base < plane; base += (size_t)(gridDim.x - 1) * EPB) {
+  for (size_t base = (size_t)blockIdx.x * EPB; base < plane; base += (size_t)nmain * EPB) {
     const size_t idx = base + e;
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
     if (idx < plane) {
@@ -1032,7 +1039,8 @@ __global__ void __launch_bounds__(256) wgrad_reduce2_kernel(const float* __restr
     }
     if (grp == 0 && idx < plane) {
       v *= scale;
-      const int co = (int)(idx % Cout), k = (int)(idx / Cout);
+      const unsigned ui = (unsigned)idx;                 // plane < 2^31 (host-checked)
+      const int co = (int)(ui % (unsigned)Cout), k = (int)(ui / (unsigned)Cout);
       int ci, tap;
       bool valid = true;
       if (first) { tap = k >> 2; ci = k & 3; valid = (tap < 9) && (ci < 3); }
@@ -1048,7 +1056,8 @@ __global__ void __launch_bounds__(256) wgrad_reduce2_kernel(const float* __restr
 static int launch_reduce2(const float* ws, const float* wsb, float* dw, float* db, int S, int Sb, int K, int Cout,
                           int Cin, int taps, int first, float beta, float scale, hipStream_t s) {
   const size_t plane = (size_t)K * Cout;
-  auto grid = [&](int epb) { return (int)std::min<size_t>((plane + epb - 1) / epb, 4096) + 1; };
+  const int nbias = (db != nullptr) ? (Cout + 15) / 16 : 0;
+  auto grid = [&](int epb) { return (int)std::min<size_t>((plane + epb - 1) / epb, 4096) + nbias; };
   if (S <= 16)
     hipLaunchKernelGGL(wgrad_reduce2_kernel<1>, dim3(grid(256)), dim3(256), 0, s, ws, wsb, dw, db, S, Sb, K, Cout,
                        Cin, taps, first, beta, scale);
@@ -1110,8 +1119,8 @@ extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, in
   const int ntile = (Cout / TCo) * ((K + TK - 1) / TK);
   // whole rounds of co-resident blocks (no half-empty last round)
   int S = target_blocks / ntile;
-  if ((cfg == 7 || cfg == 9) && getenv("CANNET_WGRAD_MANY_SLICES") == nullptr) {
-    // 8-wave 256x256 kernels run one block per CU: as few pixel slices as fill
+  if (cfg != 0 && cfg != 8 && getenv("CANNET_WGRAD_MANY_SLICES") == nullptr) {
+    // the pipelined kernels run one block per CU (LDS ring >= 128 KB): as few pixel slices as fill
     // whole rounds of the CUs to >= 90 % (fewer fp32 partial slabs to write and
     // reduce, longer K loops per block)
     static int ncu = 0;
@@ -1152,6 +1161,7 @@ extern "C" int can_conv_wgrad(const void* dy, const void* x, float* ws, float* w
   using namespace can;
   hipStream_t s = (hipStream_t)stream;
   const int K = first ? 64 : ksize * ksize * Cin;
+  if ((long long)K * Cout >= 0x7fffffffLL) return -9;   // 32-bit plane indexing in the reduction
   float* wsb_used = (db != nullptr) ? wsb : nullptr;
   int rc;
   int Sb = S;                       // bias partials summed by the reduce kernel
