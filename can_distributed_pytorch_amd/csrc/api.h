@@ -24,7 +24,7 @@ int can_head_train(const void* y, const float* w, const float* b, const float* g
 int can_sgd_momentum(float* p, float* buf, const float* g, size_t n, float lr, float momentum, float gscale,
                      int first, const float* flags, void* stream);
 int can_pack_conv(const float* w, void* fwd, void* dgr, int Co, int Ci, int taps, int first, void* stream);
-int can_pack_multi(const long long* desc, int layers, void* stream);
+int can_pack_multi(const long long* desc, int layers, int max_tiles, void* stream);
 int can_img_to_nhwc4(const float* img, void* out, int N, int H, int W, void* stream);
 
 // context.hip

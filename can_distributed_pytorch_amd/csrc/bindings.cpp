@@ -83,8 +83,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("pack_conv", [](uintptr_t w, uintptr_t fwd, uintptr_t dgr, int Co, int Ci, int taps, int first, uintptr_t st) {
     check(can_pack_conv((const float*)w, P(fwd), P(dgr), Co, Ci, taps, first, P(st)), "pack_conv");
   });
-  m.def("pack_multi", [](uintptr_t desc, int layers, uintptr_t st) {
-    check(can_pack_multi((const long long*)desc, layers, P(st)), "pack_multi");
+  m.def("pack_multi", [](uintptr_t desc, int layers, int max_tiles, uintptr_t st) {
+    check(can_pack_multi((const long long*)desc, layers, max_tiles, P(st)), "pack_multi");
   });
   m.def("img_to_nhwc4", [](uintptr_t img, uintptr_t out, int N, int H, int W, uintptr_t st) {
     check(can_img_to_nhwc4((const float*)img, P(out), N, H, W, P(st)), "img_to_nhwc4");

@@ -240,25 +240,44 @@ __global__ void __launch_bounds__(256) pack_conv_kernel(const float* __restrict_
 }
 
 // All layers' packs in one launch: blockIdx.y = layer, descriptor rows
-// {w, fwd, dgr, Co, Ci, taps, first, 0} (int64), blocks grid-stride in a layer.
+// {w, fwd, dgr, Co, Ci, taps, first, 0} (int64).  blockIdx.x = a 32(co) x
+// 32(ci) x taps tile transposed through LDS, so the fp32 reads (ci, tap
+// contiguous per co), the fwd-pack writes (ci contiguous per co, tap) and the
+// dgrad-pack writes (co contiguous per ci, tap) are all coalesced.
 __global__ void __launch_bounds__(256) pack_multi_kernel(const long long* __restrict__ desc) {
+  __shared__ unsigned short t[32][32 * 9 + 2];       // [co][ci*taps + tap] bf16 bits
   const long long* d = desc + (size_t)blockIdx.y * 8;
   const float* w = reinterpret_cast<const float*>(d[0]);
   bf16_t* fwd = reinterpret_cast<bf16_t*>(d[1]);
   bf16_t* dgr = reinterpret_cast<bf16_t*>(d[2]);
   const int Co = (int)d[3], Ci = (int)d[4], taps = (int)d[5], first = (int)d[6];
-  const size_t total = (size_t)Co * Ci * taps;
-  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
-    const int tap = i % taps;
-    const size_t r = i / taps;
-    const int ci = r % Ci;
-    const int co = r / Ci;
-    const unsigned short v = f2bf(w[i]);
-    if (first) {
-      fwd[(size_t)co * 64 + tap * 4 + ci] = v;
-    } else {
-      fwd[((size_t)co * taps + tap) * Ci + ci] = v;
-      if (dgr) dgr[((size_t)ci * taps + (taps - 1 - tap)) * Co + co] = v;
+  const int nci = (Ci + 31) / 32, nco = (Co + 31) / 32;
+  if ((int)blockIdx.x >= nci * nco) return;
+  const int co0 = (blockIdx.x / nci) * 32, ci0 = (blockIdx.x % nci) * 32;
+  const int cis = min(32, Ci - ci0), cos_ = min(32, Co - co0);
+  const int row = cis * taps;                          // contiguous floats per co in the tile
+  for (int i = threadIdx.x; i < cos_ * row; i += 256) {
+    const int c = i / row, r = i - c * row;
+    t[c][r] = f2bf(w[((size_t)(co0 + c) * Ci + ci0) * taps + r]);
+  }
+  __syncthreads();
+  if (first) {
+    for (int i = threadIdx.x; i < cos_ * row; i += 256) {
+      const int c = i / row, r = i - c * row, ci = r / taps, tap = r - ci * taps;
+      fwd[(size_t)(co0 + c) * 64 + tap * 4 + ci0 + ci] = t[c][r];
+    }
+    return;
+  }
+  // fwd[co][tap][ci]: ci fastest
+  for (int i = threadIdx.x; i < cos_ * taps * cis; i += 256) {
+    const int ci = i % cis, rest = i / cis, tap = rest % taps, c = rest / taps;
+    fwd[((size_t)(co0 + c) * taps + tap) * Ci + ci0 + ci] = t[c][ci * taps + tap];
+  }
+  if (dgr) {
+    // dgr[ci][taps-1-tap][co]: co fastest
+    for (int i = threadIdx.x; i < cis * taps * cos_; i += 256) {
+      const int c = i % cos_, rest = i / cos_, tap = rest % taps, ci = rest / taps;
+      dgr[((size_t)(ci0 + ci) * taps + (taps - 1 - tap)) * Co + co0 + c] = t[c][ci * taps + tap];
     }
   }
 }
@@ -340,8 +359,9 @@ extern "C" int can_img_to_nhwc4(const float* img, void* out, int N, int H, int W
   return (int)hipGetLastError();
 }
 
-extern "C" int can_pack_multi(const long long* desc, int layers, void* stream) {
+extern "C" int can_pack_multi(const long long* desc, int layers, int max_tiles, void* stream) {
   if (layers <= 0) return 0;
-  hipLaunchKernelGGL(pack_multi_kernel, dim3(96, layers), dim3(256), 0, (hipStream_t)stream, desc);
+  // grid.x covers the largest layer's 32x32 tiles (B1: 512 -> 1024 channels = 512 tiles)
+  hipLaunchKernelGGL(pack_multi_kernel, dim3(max_tiles, layers), dim3(256), 0, (hipStream_t)stream, desc);
   return (int)hipGetLastError();
 }

@@ -141,6 +141,7 @@ class CANNetExecutor:
                 rows.append([self.ctx2[sc].weight.data_ptr(), fwd.data_ptr(), dgr.data_ptr(), 512, 512, 1, 0, 0])
             self._pack_desc = torch.tensor(rows, dtype=torch.int64, device=dev)
             self._pack_desc_ptrs = tuple(r[0] for r in rows)
+            self._pack_tiles = max(((r[3] + 31) // 32) * ((r[4] + 31) // 32) for r in rows)
         # one launch for every layer (descriptor rows hold the fp32 master pointers,
         # which the flat arena keeps fixed; rebuilt if a weight tensor moved)
         cur = tuple(s.module.weight.data_ptr() for s in self.front + self.back) + \
@@ -148,7 +149,7 @@ class CANNetExecutor:
         if cur != self._pack_desc_ptrs:
             self._pack_desc = None
             return self.refresh_packs(force=True)
-        self.C.pack_multi(self._pack_desc.data_ptr(), self._pack_desc.shape[0], st)
+        self.C.pack_multi(self._pack_desc.data_ptr(), self._pack_desc.shape[0], self._pack_tiles, st)
         self._pack_version = ver
 
     def mark_weights_updated(self):

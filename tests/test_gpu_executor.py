@@ -144,3 +144,28 @@ def test_native_stepper_with_rccl_reducer_world1(graph):
     torch.cuda.synchronize()
     for pa, pb in zip(nat_a.parameters(), nat_b.parameters()):
         assert torch.equal(pa, pb)
+
+
+def test_batched_packs_match_reference_packing():
+    """The one-launch LDS-transposing pack kernel reproduces the Python reference packs bit for bit."""
+    from can_distributed_pytorch_amd.models.cannet import CANNet
+    from can_distributed_pytorch_amd.ops import conv as C
+    from can_distributed_pytorch_amd.ops.executor import CANNetExecutor
+    torch.manual_seed(7)
+    model = CANNet(backend="hip").cuda()
+    ex = CANNetExecutor(model)
+    ex.refresh_packs(force=True)
+    torch.cuda.synchronize()
+    for s in ex.front + ex.back:
+        w = s.module.weight.detach()
+        fwd, dgr = ex.packs[id(s.module.weight)]
+        if s.first:
+            assert torch.equal(fwd, C.pack_weight_first(w))
+        else:
+            assert torch.equal(fwd, C.pack_weight_fwd(w)), s
+            assert torch.equal(dgr, C.pack_weight_dgrad(w)), s
+    for sc, conv in ex.ctx2.items():
+        fwd, dgr = ex.packs[id(conv.weight)]
+        w = conv.weight.detach()
+        assert torch.equal(fwd, C.pack_weight_fwd(w))
+        assert torch.equal(dgr, C.pack_weight_dgrad(w))
