@@ -928,6 +928,7 @@ static int dispatch_glds(const ConvArgs2& a, int tile_cfg, hipStream_t s) {
     case 21: if (a.Cout % 256) return -8; return launch_glds2<4, 2, 2, EPI>(a, s);
     case 22: if (a.Cout % 128) return -8; return launch_glds2<2, 4, 1, EPI>(a, s);
     case 23: return launch_glds2<1, 8, 1, EPI>(a, s);
+    case 25: if (a.Cout % 128) return -8; return launch_glds2<2, 4, 2, EPI>(a, s);   // 128 x 512, 160 KB LDS
   }
   return -9;
 }

@@ -64,7 +64,8 @@ def main():
         db = torch.empty(co, device=dev)
         res = {"layer": name, "shape": [n, h, w, ci, co, dil], "gflop": fl / 1e9}
         # --tile >= 20: the v2 kernel with the tile that fits the channel count
-        pick = (lambda c: (21 if c % 256 == 0 else 22 if c % 128 == 0 else 23) if a.tile >= 20 else a.tile)
+        pick = (lambda c: (21 if c % 256 == 0 else (25 if a.tile == 25 else 22) if c % 128 == 0 else 23)
+                if a.tile >= 20 else a.tile)
         t, td = pick(co), pick(ci)
         if a.halo and ci == 64 and dil == 1 and co in (64, 128):
             t = 31

@@ -35,6 +35,8 @@ def _close(a, b, tol=2e-2):
     # halo-tiled Cin = 64 kernel: full tiles, ragged rows / columns, Cout 64 and 128
     (1, 4, 128, 64, 64, 3, 1, 31), (2, 10, 200, 64, 64, 3, 1, 31), (1, 9, 130, 64, 128, 3, 1, 31),
     (2, 3, 7, 64, 128, 3, 1, 31),
+    # 128 x 512 tile (160 KB LDS)
+    (1, 20, 40, 128, 128, 3, 1, 25), (2, 9, 13, 256, 128, 3, 2, 25), (1, 5, 7, 128, 384, 1, 1, 25),
 ])
 def test_conv_fwd(n, h, w, ci, co, k, dil, tile):
     from can_distributed_pytorch_amd.ops import conv as C
