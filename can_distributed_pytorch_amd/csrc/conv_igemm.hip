@@ -690,7 +690,7 @@ __global__ void __launch_bounds__(512, 1) conv_halo64_kernel(HaloConvArgs a) {
     const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
     const void* src = a.zero;
     if (hp < HPIX && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
-      src = a.x + ((size_t)(n * a.H + ih) * a.W + iw) * 64 + (((lane & 7) ^ (hp & 7)) * 8);
+      src = a.x + ((size_t)(n * a.H + ih) * a.W + iw) * 64 + (((lane & 7) ^ (hc & 7)) * 8);
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(halo + i * 1024), 16, 0, 0);
   }
   auto issue_w = [&](int t) {
@@ -716,30 +716,37 @@ __global__ void __launch_bounds__(512, 1) conv_halo64_kernel(HaloConvArgs a) {
 #pragma unroll
     for (int i = 0; i < 4 * PW; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // Per-lane LDS byte offsets, loop invariant: the halo swizzle is keyed by the
+  // halo COLUMN (hc & 7 = (fr + kw) & 7 for every fragment and row), so each
+  // fragment read is one ds_read_b128 at lane offset + compile-time immediate.
   const int fr = lane & 15, fq = lane >> 4;
+  int hoff[3][2], woff[2];
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+      hoff[kw][kk] = (r * HC + colbase + fr + kw) * 128 + (((kk * 4 + fq) ^ ((fr + kw) & 7)) * 16);
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) woff[kk] = (wc * 64 + fr) * 128 + (((kk * 4 + fq) ^ (fr & 7)) * 16);
+#pragma unroll
   for (int t = 0; t < 9; ++t) {
     // tap t's weights (and, for t = 0, the halo) have landed; the ring slot of
     // tap t-1 is free once every wave is past this barrier
     if (t + 1 < 9) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" :: "n"(GW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     if (t + 2 < 9) issue_w(t + 2);
-    const int kh = (t * 11) >> 5, kw = t - kh * 3;
-    const uint4* As = reinterpret_cast<const uint4*>(wring + (t % 3) * WTAP);
-    const uint4* Hs = reinterpret_cast<const uint4*>(halo);
+    const int kh = t / 3, kw = t % 3;
+    const unsigned char* Ab = wring + (t % 3) * WTAP;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const int chunk = kk * 4 + fq;
       bf16x8_t af[4], bfr[4 * PW];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = wc * 64 + j * 16 + fr;
-        af[j] = __builtin_bit_cast(bf16x8_t, As[row * 8 + swz(row, chunk)]);
-      }
+      for (int j = 0; j < 4; ++j)
+        af[j] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(Ab + woff[kk] + j * 2048));
 #pragma unroll
-      for (int i = 0; i < 4 * PW; ++i) {
-        const int hp = (r + kh) * HC + colbase + i * 16 + fr + kw;
-        bfr[i] = __builtin_bit_cast(bf16x8_t, Hs[hp * 8 + (chunk ^ (hp & 7))]);
-      }
+      for (int i = 0; i < 4 * PW; ++i)
+        bfr[i] = __builtin_bit_cast(bf16x8_t,
+                                    *reinterpret_cast<const uint4*>(halo + hoff[kw][kk] + kh * HC * 128 + i * 2048));
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -920,7 +927,10 @@ static int launch_glds(const ConvArgs2& a, hipStream_t s) {
 template <int EPI>
 static int dispatch_glds(const ConvArgs2& a, int tile_cfg, hipStream_t s) {
   int cfg = tile_cfg;
-  if (cfg == 0) cfg = (a.Cout % 256 == 0) ? 21 : (a.Cout % 128 == 0) ? 22 : 23;   // v2 (pipelined) by default
+  if (cfg == 0) {   // v2 (pipelined) by default; 128 x 512 tiles measured faster for K <= 1152
+    const int ktot = a.ksize * a.ksize * a.Cin;
+    cfg = (a.Cout % 256 == 0) ? 21 : (a.Cout % 128 == 0) ? (ktot <= 1152 ? 25 : 22) : 23;
+  }
   switch (cfg) {
     case 11: if (a.Cout % 256) return -8; return launch_glds<4, 2, 2, EPI>(a, s);
     case 12: if (a.Cout % 128) return -8; return launch_glds<2, 4, 1, EPI>(a, s);
