@@ -1,5 +1,6 @@
 // C ABI of the HIP kernel translation units (one launcher per kernel family).
 // Return value: 0 ok, >0 hipError_t, <0 argument/shape error.
+// dt selects the 16-bit element type of activations / weight packs: 0 = bf16, 1 = fp16.
 #pragma once
 #include <stdint.h>
 #ifdef __cplusplus
@@ -7,41 +8,51 @@ extern "C" {
 #endif
 
 int can_conv_igemm(const void* x, const void* w, const float* bias, const void* mask, void* y, int N, int H, int W,
-                   int Cin, int Cout, int ksize, int dil, int epi, int first, int tile_cfg, void* stream);
+                   int Cin, int Cout, int ksize, int dil, int epi, int first, int tile_cfg, int dt, void* stream);
 
 int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, int target_blocks, int* S_out, int* mslice_out,
                    int* cfg_out);
 int can_conv_wgrad(const void* dy, const void* x, float* ws, float* wsb, float* dw, float* db, int N, int H, int W,
                    int Cin, int Cout, int ksize, int dil, int first, int S, int mslice, int cfg, float beta,
-                   float scale, void* stream);
+                   float scale, const float* dscale, int dt, void* stream);
+
+int can_conv_wgrad_1x1_batched(const void* dy, const void* x, float* ws, float* dw, int M, int W, int Cin, int Cout,
+                               int nb, long long dy_bs, long long x_bs, long long dw_bs, int S, int mslice, float beta,
+                               float scale, const float* dscale, int dt, void* stream);
 
 // elementwise.hip
-int can_maxpool_fwd(const void* x, void* y, int N, int H, int W, int C, void* stream);
-int can_maxpool_bwd_relu(const void* x, const void* dy, void* dx, int N, int H, int W, int C, void* stream);
-int can_head_fwd(const void* y, const float* w, const float* b, float* et, int P, void* stream);
+int can_maxpool_fwd(const void* x, void* y, int N, int H, int W, int C, int dt, void* stream);
+int can_maxpool_bwd_relu(const void* x, const void* dy, void* dx, int N, int H, int W, int C, int dt, void* stream);
+int can_head_fwd(const void* y, const float* w, const float* b, float* et, int P, int dt, void* stream);
 int can_head_train(const void* y, const float* w, const float* b, const float* gt, float* et, void* dy, float* part,
-                   int nblk, float* dw, float* db, float* loss, int P, float gscale, float beta, void* stream);
+                   int nblk, float* dw, float* db, float* loss, int P, float gscale, float beta, const float* lscale,
+                   int dt, void* stream);
 int can_sgd_momentum(float* p, float* buf, const float* g, size_t n, float lr, float momentum, float gscale,
                      int first, const float* flags, void* stream);
-int can_pack_conv(const float* w, void* fwd, void* dgr, int Co, int Ci, int taps, int first, void* stream);
-int can_pack_multi(const long long* desc, int layers, int max_tiles, void* stream);
-int can_img_to_nhwc4(const float* img, void* out, int N, int H, int W, void* stream);
+int can_grad_nonfinite(const float* g, size_t n, float* flags, void* stream);
+int can_scale_update(const float* flags, float* scaler, int interval, float growth, float backoff, float max_scale,
+                     void* stream);
+int can_pack_conv(const float* w, void* fwd, void* dgr, int Co, int Ci, int taps, int first, int dt, void* stream);
+int can_pack_multi(const long long* desc, int layers, int max_tiles, int dt, void* stream);
+int can_img_to_nhwc4(const float* img, void* out, int N, int H, int W, int dt, void* stream);
 
 // context.hip
 int can_ctx_reduce(int mode, const void* in0, const void* sdir, const void* dc, float* rowacc, float* cells, int N,
-                   int h, int w, int C, void* stream);
-int can_ctx_expand(const void* fv, const float* T, void* cs, int N, int h, int w, int C, void* stream);
-int can_ctx_fuse(const void* fv, const void* ws, const float* T, void* cat, int N, int h, int w, int C, void* stream);
+                   int h, int w, int C, int dt, void* stream);
+int can_ctx_expand(const void* fv, const float* T, void* cs, int N, int h, int w, int C, int dt, void* stream);
+int can_ctx_fuse(const void* fv, const void* ws, const float* T, void* cat, int N, int h, int w, int C, int dt,
+                 void* stream);
 int can_ctx_bwd_e1(const void* dcat, const void* ws, const float* T, void* dz, void* sdir, int N, int h, int w, int C,
-                   void* stream);
+                   int dt, void* stream);
 int can_ctx_bwd_final(const void* dcat, const void* dc, const float* dave, const void* fv, void* dfv, int N, int h,
-                      int w, int C, void* stream);
+                      int w, int C, int dt, void* stream);
 
 // density.hip
 int can_density_map(const float* pts, int n, int H, int W, float* sigma_ws, float* out, int max_r, void* stream);
 
 // preprocess.hip
-int can_preprocess_image(const void* img, int H0, int W0, int C, int flip, void* out, int Ho, int Wo, void* stream);
+int can_preprocess_image(const void* img, int H0, int W0, int C, int flip, void* out, int Ho, int Wo, int dt,
+                         void* stream);
 int can_preprocess_density(const float* d, int H0, int W0, int flip, float* out, int Ho, int Wo, float mult,
                            void* stream);
 

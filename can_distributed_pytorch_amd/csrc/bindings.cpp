@@ -38,9 +38,9 @@ PYBIND11_MODULE(_C, m) {
   });
 
   m.def("conv_igemm", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t mask, uintptr_t y, int N, int H, int W,
-                         int Cin, int Cout, int ksize, int dil, int epi, int first, int tile_cfg, uintptr_t stream) {
+                         int Cin, int Cout, int ksize, int dil, int epi, int first, int tile_cfg, int dt, uintptr_t stream) {
     check(can_conv_igemm(P(x), P(w), (const float*)bias, P(mask), P(y), N, H, W, Cin, Cout, ksize, dil, epi, first,
-                         tile_cfg, P(stream)),
+                         tile_cfg, dt, P(stream)),
           "conv_igemm");
   });
 
@@ -51,27 +51,37 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("conv_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t ws, uintptr_t wsb, uintptr_t dw, uintptr_t db, int N,
                          int H, int W, int Cin, int Cout, int ksize, int dil, int first, int S, int mslice, int cfg,
-                         float beta, float scale, uintptr_t stream) {
+                         float beta, float scale, uintptr_t dscale, int dt, uintptr_t stream) {
     check(can_conv_wgrad(P(dy), P(x), (float*)ws, (float*)wsb, (float*)dw, (float*)db, N, H, W, Cin, Cout, ksize, dil,
-                         first, S, mslice, cfg, beta, scale, P(stream)),
+                         first, S, mslice, cfg, beta, scale, (const float*)dscale, dt, P(stream)),
           "conv_wgrad");
   });
 
+  m.def("conv_wgrad_1x1_batched", [](uintptr_t dy, uintptr_t x, uintptr_t ws, uintptr_t dw, int M, int W, int Cin,
+                                     int Cout, int nb, long long dy_bs, long long x_bs, long long dw_bs, int S,
+                                     int mslice, float beta, float scale, uintptr_t dscale, int dt, uintptr_t stream) {
+    check(can_conv_wgrad_1x1_batched(P(dy), P(x), (float*)ws, (float*)dw, M, W, Cin, Cout, nb, dy_bs, x_bs, dw_bs, S,
+                                     mslice, beta, scale, (const float*)dscale, dt, P(stream)),
+          "conv_wgrad_1x1_batched");
+  });
+
   // ---- elementwise
-  m.def("maxpool_fwd", [](uintptr_t x, uintptr_t y, int N, int H, int W, int C, uintptr_t st) {
-    check(can_maxpool_fwd(P(x), P(y), N, H, W, C, P(st)), "maxpool_fwd");
+  m.def("maxpool_fwd", [](uintptr_t x, uintptr_t y, int N, int H, int W, int C, int dt, uintptr_t st) {
+    check(can_maxpool_fwd(P(x), P(y), N, H, W, C, dt, P(st)), "maxpool_fwd");
   });
-  m.def("maxpool_bwd_relu", [](uintptr_t x, uintptr_t dy, uintptr_t dx, int N, int H, int W, int C, uintptr_t st) {
-    check(can_maxpool_bwd_relu(P(x), P(dy), P(dx), N, H, W, C, P(st)), "maxpool_bwd_relu");
+  m.def("maxpool_bwd_relu", [](uintptr_t x, uintptr_t dy, uintptr_t dx, int N, int H, int W, int C, int dt,
+                               uintptr_t st) {
+    check(can_maxpool_bwd_relu(P(x), P(dy), P(dx), N, H, W, C, dt, P(st)), "maxpool_bwd_relu");
   });
-  m.def("head_fwd", [](uintptr_t y, uintptr_t w, uintptr_t b, uintptr_t et, int Pn, uintptr_t st) {
-    check(can_head_fwd(P(y), (const float*)w, (const float*)b, (float*)et, Pn, P(st)), "head_fwd");
+  m.def("head_fwd", [](uintptr_t y, uintptr_t w, uintptr_t b, uintptr_t et, int Pn, int dt, uintptr_t st) {
+    check(can_head_fwd(P(y), (const float*)w, (const float*)b, (float*)et, Pn, dt, P(st)), "head_fwd");
   });
   m.def("head_train", [](uintptr_t y, uintptr_t w, uintptr_t b, uintptr_t gt, uintptr_t et, uintptr_t dy,
                          uintptr_t part, int nblk, uintptr_t dw, uintptr_t db, uintptr_t loss, int Pn, float gscale,
-                         float beta, uintptr_t st) {
+                         float beta, uintptr_t lscale, int dt, uintptr_t st) {
     check(can_head_train(P(y), (const float*)w, (const float*)b, (const float*)gt, (float*)et, P(dy), (float*)part,
-                         nblk, (float*)dw, (float*)db, (float*)loss, Pn, gscale, beta, P(st)),
+                         nblk, (float*)dw, (float*)db, (float*)loss, Pn, gscale, beta, (const float*)lscale, dt,
+                         P(st)),
           "head_train");
   });
   m.def("sgd_momentum", [](uintptr_t p, uintptr_t buf, uintptr_t g, size_t n, float lr, float mom, float gscale,
@@ -80,44 +90,54 @@ PYBIND11_MODULE(_C, m) {
                            P(st)),
           "sgd_momentum");
   });
-  m.def("pack_conv", [](uintptr_t w, uintptr_t fwd, uintptr_t dgr, int Co, int Ci, int taps, int first, uintptr_t st) {
-    check(can_pack_conv((const float*)w, P(fwd), P(dgr), Co, Ci, taps, first, P(st)), "pack_conv");
+  m.def("grad_nonfinite", [](uintptr_t g, size_t n, uintptr_t flags, uintptr_t st) {
+    check(can_grad_nonfinite((const float*)g, n, (float*)flags, P(st)), "grad_nonfinite");
   });
-  m.def("pack_multi", [](uintptr_t desc, int layers, int max_tiles, uintptr_t st) {
-    check(can_pack_multi((const long long*)desc, layers, max_tiles, P(st)), "pack_multi");
+  m.def("scale_update", [](uintptr_t flags, uintptr_t scaler, int interval, float growth, float backoff, float max_scale,
+                           uintptr_t st) {
+    check(can_scale_update((const float*)flags, (float*)scaler, interval, growth, backoff, max_scale, P(st)),
+          "scale_update");
   });
-  m.def("img_to_nhwc4", [](uintptr_t img, uintptr_t out, int N, int H, int W, uintptr_t st) {
-    check(can_img_to_nhwc4((const float*)img, P(out), N, H, W, P(st)), "img_to_nhwc4");
+  m.def("pack_conv", [](uintptr_t w, uintptr_t fwd, uintptr_t dgr, int Co, int Ci, int taps, int first, int dt,
+                        uintptr_t st) {
+    check(can_pack_conv((const float*)w, P(fwd), P(dgr), Co, Ci, taps, first, dt, P(st)), "pack_conv");
+  });
+  m.def("pack_multi", [](uintptr_t desc, int layers, int max_tiles, int dt, uintptr_t st) {
+    check(can_pack_multi((const long long*)desc, layers, max_tiles, dt, P(st)), "pack_multi");
+  });
+  m.def("img_to_nhwc4", [](uintptr_t img, uintptr_t out, int N, int H, int W, int dt, uintptr_t st) {
+    check(can_img_to_nhwc4((const float*)img, P(out), N, H, W, dt, P(st)), "img_to_nhwc4");
   });
   // ---- context module
   m.def("ctx_reduce", [](int mode, uintptr_t in0, uintptr_t sdir, uintptr_t dc, uintptr_t rowacc, uintptr_t cells,
-                         int N, int h, int w, int C, uintptr_t st) {
-    check(can_ctx_reduce(mode, P(in0), P(sdir), P(dc), (float*)rowacc, (float*)cells, N, h, w, C, P(st)),
+                         int N, int h, int w, int C, int dt, uintptr_t st) {
+    check(can_ctx_reduce(mode, P(in0), P(sdir), P(dc), (float*)rowacc, (float*)cells, N, h, w, C, dt, P(st)),
           "ctx_reduce");
   });
-  m.def("ctx_expand", [](uintptr_t fv, uintptr_t T, uintptr_t cs, int N, int h, int w, int C, uintptr_t st) {
-    check(can_ctx_expand(P(fv), (const float*)T, P(cs), N, h, w, C, P(st)), "ctx_expand");
+  m.def("ctx_expand", [](uintptr_t fv, uintptr_t T, uintptr_t cs, int N, int h, int w, int C, int dt, uintptr_t st) {
+    check(can_ctx_expand(P(fv), (const float*)T, P(cs), N, h, w, C, dt, P(st)), "ctx_expand");
   });
-  m.def("ctx_fuse", [](uintptr_t fv, uintptr_t ws, uintptr_t T, uintptr_t cat, int N, int h, int w, int C,
+  m.def("ctx_fuse", [](uintptr_t fv, uintptr_t ws, uintptr_t T, uintptr_t cat, int N, int h, int w, int C, int dt,
                        uintptr_t st) {
-    check(can_ctx_fuse(P(fv), P(ws), (const float*)T, P(cat), N, h, w, C, P(st)), "ctx_fuse");
+    check(can_ctx_fuse(P(fv), P(ws), (const float*)T, P(cat), N, h, w, C, dt, P(st)), "ctx_fuse");
   });
   m.def("ctx_bwd_e1", [](uintptr_t dcat, uintptr_t ws, uintptr_t T, uintptr_t dz, uintptr_t sdir, int N, int h, int w,
-                         int C, uintptr_t st) {
-    check(can_ctx_bwd_e1(P(dcat), P(ws), (const float*)T, P(dz), P(sdir), N, h, w, C, P(st)), "ctx_bwd_e1");
+                         int C, int dt, uintptr_t st) {
+    check(can_ctx_bwd_e1(P(dcat), P(ws), (const float*)T, P(dz), P(sdir), N, h, w, C, dt, P(st)), "ctx_bwd_e1");
   });
   m.def("ctx_bwd_final", [](uintptr_t dcat, uintptr_t dc, uintptr_t dave, uintptr_t fv, uintptr_t dfv, int N, int h,
-                            int w, int C, uintptr_t st) {
-    check(can_ctx_bwd_final(P(dcat), P(dc), (const float*)dave, P(fv), P(dfv), N, h, w, C, P(st)), "ctx_bwd_final");
+                            int w, int C, int dt, uintptr_t st) {
+    check(can_ctx_bwd_final(P(dcat), P(dc), (const float*)dave, P(fv), P(dfv), N, h, w, C, dt, P(st)),
+          "ctx_bwd_final");
   });
   // ---- density maps
   m.def("density_map", [](uintptr_t pts, int n, int H, int W, uintptr_t sig, uintptr_t out, int max_r, uintptr_t st) {
     check(can_density_map((const float*)pts, n, H, W, (float*)sig, (float*)out, max_r, P(st)), "density_map");
   });
   // ---- input pipeline
-  m.def("preprocess_image", [](uintptr_t img, int H0, int W0, int C, int flip, uintptr_t out, int Ho, int Wo,
+  m.def("preprocess_image", [](uintptr_t img, int H0, int W0, int C, int flip, uintptr_t out, int Ho, int Wo, int dt,
                                uintptr_t st) {
-    check(can_preprocess_image(P(img), H0, W0, C, flip, P(out), Ho, Wo, P(st)), "preprocess_image");
+    check(can_preprocess_image(P(img), H0, W0, C, flip, P(out), Ho, Wo, dt, P(st)), "preprocess_image");
   });
   m.def("preprocess_density", [](uintptr_t d, int H0, int W0, int flip, uintptr_t out, int Ho, int Wo, float mult,
                                  uintptr_t st) {

@@ -33,6 +33,98 @@ __device__ __forceinline__ unsigned pack2bf(float lo, float hi) {
   return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
 }
 
+// ---------------------------------------------------------------------------
+// 16-bit activation / weight-pack element types.  Every NHWC activation, packed
+// weight and MFMA operand of the network is one of these two (selected per
+// launch from the tensors' dtype); accumulation, master weights, gradients
+// slabs and optimizer state are always fp32.  Kernels move the raw 16-bit
+// words (LDS-DMA, transposed LDS reads) type-blind; only the MFMA instruction,
+// the constant 1.0 and the fp32 <-> 16-bit conversions depend on the type.
+// ---------------------------------------------------------------------------
+enum { DT_BF16 = 0, DT_F16 = 1 };
+
+typedef __bf16 frag8_t __attribute__((ext_vector_type(8)));     // 8 x 16-bit MFMA operand (bits)
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+
+template <int DT>
+__device__ __forceinline__ f32x4 mfma16(const frag8_t& a, const frag8_t& b, const f32x4& c) {
+  if constexpr (DT == DT_F16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c,
+                                                  0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// bit pattern of 1.0
+template <int DT>
+__device__ __forceinline__ constexpr unsigned short one_bits() { return DT == DT_F16 ? 0x3C00 : 0x3F80; }
+template <int DT>
+__device__ __forceinline__ frag8_t ones_frag() {
+  const short o = (short)one_bits<DT>();
+  typedef short s16x8_ __attribute__((ext_vector_type(8)));
+  const s16x8_ v = {o, o, o, o, o, o, o, o};
+  return __builtin_bit_cast(frag8_t, v);
+}
+template <int DT>
+__device__ __forceinline__ float h2f(unsigned short v) {
+  if constexpr (DT == DT_F16) return (float)__builtin_bit_cast(_Float16, v);
+  else return bf2f(v);
+}
+template <int DT>
+__device__ __forceinline__ unsigned short f2h(float f) {
+  if constexpr (DT == DT_F16) return __builtin_bit_cast(unsigned short, (_Float16)f);   // RNE, +-inf on overflow
+  else return f2bf(f);
+}
+template <int DT>
+__device__ __forceinline__ unsigned pack2(float lo, float hi) {
+  return (unsigned)f2h<DT>(lo) | ((unsigned)f2h<DT>(hi) << 16);
+}
+// 8 packed 16-bit values (one 16-B vector) <-> 8 floats
+template <int DT>
+__device__ __forceinline__ void unpack8h(const uint4& v, float* f) {
+  const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if constexpr (DT == DT_F16) {
+      f[2 * i] = h2f<DT>((unsigned short)(w[i] & 0xffffu));
+      f[2 * i + 1] = h2f<DT>((unsigned short)(w[i] >> 16));
+    } else {
+      f[2 * i] = __uint_as_float(w[i] << 16);
+      f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+}
+template <int DT>
+__device__ __forceinline__ uint4 pack8h(const float* f) {
+  return make_uint4(pack2<DT>(f[0], f[1]), pack2<DT>(f[2], f[3]), pack2<DT>(f[4], f[5]), pack2<DT>(f[6], f[7]));
+}
+// x > 0 on the raw bits (same test for both types: sign clear, not +0)
+__device__ __forceinline__ bool pos_bits(unsigned short b) { return ((b & 0x8000u) == 0) && ((b & 0x7fffu) != 0); }
+
+// Dispatch a launcher templated on the element type: CAN_DT(dt, F<DT>(args)).
+#define CAN_DT_DISPATCH(dt, ...)                                 \
+  do {                                                           \
+    if ((dt) == ::can::DT_F16) {                                 \
+      constexpr int DT = ::can::DT_F16;                          \
+      return __VA_ARGS__;                                        \
+    } else if ((dt) == ::can::DT_BF16) {                         \
+      constexpr int DT = ::can::DT_BF16;                         \
+      return __VA_ARGS__;                                        \
+    }                                                            \
+    return -20;                                                  \
+  } while (0)
+
+// Launch kernel template K<DT> for a runtime element type (returns -20 from the
+// enclosing function on an unknown dt).
+#define CAN_LAUNCH_DT(dt, K, ...)                                  \
+  do {                                                             \
+    if ((dt) == ::can::DT_F16)                                     \
+      hipLaunchKernelGGL(K<::can::DT_F16>, __VA_ARGS__);           \
+    else if ((dt) == ::can::DT_BF16)                               \
+      hipLaunchKernelGGL(K<::can::DT_BF16>, __VA_ARGS__);          \
+    else                                                           \
+      return -20;                                                  \
+  } while (0)
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -28,18 +28,6 @@ __constant__ int kScale[4] = {1, 2, 3, 6};
 __constant__ int kCellOff[4] = {0, 1, 5, 14};
 __constant__ int kBinOff[4] = {0, 1, 3, 6};
 
-__device__ __forceinline__ void unpack8c(const uint4& v, float* f) {
-  const unsigned w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    f[2 * i] = __uint_as_float(w[i] << 16);
-    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
-  }
-}
-__device__ __forceinline__ uint4 pack8c(const float* f) {
-  return make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
-}
-
 // adaptive-avg-pool bin [start,end) of index i at scale S over length L
 __device__ __forceinline__ void pool_bin(int i, int S, int L, int& st, int& en) {
   st = (i * L) / S;
@@ -81,7 +69,7 @@ __device__ __forceinline__ void bil(int S, int x, int L, int& x0, int& x1, float
 // column segments over adjacent lanes (thread = cg*4 + seg), the 4 partial
 // sums are combined with lane shuffles (fixed order), and each lane stores 3
 // of the 12 bins.  The 12 x w bin weights are tabulated once per block in LDS.
-template <bool POOL>
+template <int DT, bool POOL>
 __global__ void __launch_bounds__(256) ctx_rows_kernel(const uint4* __restrict__ in0, const uint4* __restrict__ sdir,
                                                        const uint4* __restrict__ dc, float* __restrict__ rowacc,
                                                        int N, int h, int w, int C) {
@@ -112,7 +100,7 @@ __global__ void __launch_bounds__(256) ctx_rows_kernel(const uint4* __restrict__
       const size_t pix = ny * w + x;
       if (POOL) {
         float v[8];
-        unpack8c(in0[pix * C8 + cg], v);
+        unpack8h<DT>(in0[pix * C8 + cg], v);
 #pragma unroll
         for (int b = 0; b < 12; ++b) {
           const float wt = wtab[b * w + x];
@@ -125,8 +113,8 @@ __global__ void __launch_bounds__(256) ctx_rows_kernel(const uint4* __restrict__
           const int S = (si == 0) ? 1 : (si == 1) ? 2 : (si == 2) ? 3 : 6;
           const int bo = (si == 0) ? 0 : (si == 1) ? 1 : (si == 2) ? 3 : 6;
           float v[8], u[8];
-          unpack8c(sdir[(size_t)si * P * C8 + pix * C8 + cg], v);
-          unpack8c(dc[(size_t)si * P * C8 + pix * C8 + cg], u);
+          unpack8h<DT>(sdir[(size_t)si * P * C8 + pix * C8 + cg], v);
+          unpack8h<DT>(dc[(size_t)si * P * C8 + pix * C8 + cg], u);
 #pragma unroll
           for (int k = 0; k < 8; ++k) v[k] += u[k];
 #pragma unroll
@@ -304,6 +292,7 @@ __device__ __forceinline__ RowRun row_run(int h, int w, int C8) {
 }
 
 // c_S = up_S - fv for the 4 scales: cs[si][P][C] bf16
+template <int DT>
 __global__ void __launch_bounds__(256) ctx_expand_kernel(const uint4* __restrict__ fv, const float* __restrict__ T,
                                                          uint4* __restrict__ cs, int N, int h, int w, int C) {
   const int C8 = C >> 3;
@@ -315,16 +304,17 @@ __global__ void __launch_bounds__(256) ctx_expand_kernel(const uint4* __restrict
   for (int x = r.x0; x < r.x1; ++x) {
     const size_t t = (r.ny * w + x) * C8 + r.cg;
     float f[8];
-    unpack8c(fv[t], f);
+    unpack8h<DT>(fv[t], f);
     up_all(R, x, w, [&](int si, float* u) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) u[k] -= f[k];
-      cs[(size_t)si * total + t] = pack8c(u);
+      cs[(size_t)si * total + t] = pack8h<DT>(u);
     });
   }
 }
 
 // cat[p] = [fv | fi],  fi = sum w_S s_S / (sum w_S + 1e-12)
+template <int DT>
 __global__ void __launch_bounds__(256) ctx_fuse_kernel(const uint4* __restrict__ fv, const uint4* __restrict__ ws,
                                                        const float* __restrict__ T, uint4* __restrict__ cat, int N,
                                                        int h, int w, int C) {
@@ -342,18 +332,19 @@ __global__ void __launch_bounds__(256) ctx_fuse_kernel(const uint4* __restrict__
     for (int k = 0; k < 8; ++k) { num[k] = 0.f; den[k] = 0.f; }
     up_all(R, x, w, [&](int si, float* u) {
       float wv[8];
-      unpack8c(ws[(size_t)si * total + t], wv);
+      unpack8h<DT>(ws[(size_t)si * total + t], wv);
 #pragma unroll
       for (int k = 0; k < 8; ++k) { num[k] += wv[k] * u[k]; den[k] += wv[k]; }
     });
 #pragma unroll
     for (int k = 0; k < 8; ++k) num[k] = num[k] / (den[k] + 1e-12f);
     cat[p * 2 * C8 + r.cg] = fv[t];
-    cat[p * 2 * C8 + C8 + r.cg] = pack8c(num);
+    cat[p * 2 * C8 + C8 + r.cg] = pack8h<DT>(num);
   }
 }
 
 // backward elementwise: dz_S and sdir_S for the 4 scales
+template <int DT>
 __global__ void __launch_bounds__(256) ctx_bwd_e1_kernel(const uint4* __restrict__ dcat, const uint4* __restrict__ ws,
                                                          const float* __restrict__ T, uint4* __restrict__ dz,
                                                          uint4* __restrict__ sdir, int N, int h, int w, int C) {
@@ -370,11 +361,11 @@ __global__ void __launch_bounds__(256) ctx_bwd_e1_kernel(const uint4* __restrict
 #pragma unroll
     for (int k = 0; k < 8; ++k) { num[k] = 0.f; den[k] = 0.f; }
     up_all(R, x, w, [&](int si, float* u) {
-      unpack8c(ws[(size_t)si * total + t], wv[si]);
+      unpack8h<DT>(ws[(size_t)si * total + t], wv[si]);
 #pragma unroll
       for (int k = 0; k < 8; ++k) { s[si][k] = u[k]; num[k] += wv[si][k] * u[k]; den[k] += wv[si][k]; }
     });
-    unpack8c(dcat[p * 2 * C8 + C8 + r.cg], dfi);
+    unpack8h<DT>(dcat[p * 2 * C8 + C8 + r.cg], dfi);
 #pragma unroll
     for (int k = 0; k < 8; ++k) { den[k] += 1e-12f; num[k] = num[k] / den[k]; }   // num := fi
 #pragma unroll
@@ -387,8 +378,8 @@ __global__ void __launch_bounds__(256) ctx_bwd_e1_kernel(const uint4* __restrict
         a[k] = dws * wv[si][k] * (1.f - wv[si][k]);
         b[k] = g * wv[si][k];
       }
-      dz[(size_t)si * total + t] = pack8c(a);
-      sdir[(size_t)si * total + t] = pack8c(b);
+      dz[(size_t)si * total + t] = pack8h<DT>(a);
+      sdir[(size_t)si * total + t] = pack8h<DT>(b);
     }
   }
 }
@@ -397,6 +388,7 @@ __global__ void __launch_bounds__(256) ctx_bwd_e1_kernel(const uint4* __restrict
 // pool^T: the row's pooled-cell gradients (bins containing y, divided by the
 // bin height) are summed once per thread into a RowTab; per column the bins
 // containing x contribute / bin width.
+template <int DT>
 __global__ void __launch_bounds__(256) ctx_bwd_final_kernel(const uint4* __restrict__ dcat,
                                                             const uint4* __restrict__ dc, const float* __restrict__ dave,
                                                             const uint4* __restrict__ fv, uint4* __restrict__ dfv,
@@ -439,10 +431,10 @@ __global__ void __launch_bounds__(256) ctx_bwd_final_kernel(const uint4* __restr
     const size_t p = r.ny * w + x;
     const size_t t = p * C8 + r.cg;
     float g[8], u[8];
-    unpack8c(dcat[p * 2 * C8 + r.cg], g);
+    unpack8h<DT>(dcat[p * 2 * C8 + r.cg], g);
 #pragma unroll
     for (int si = 0; si < 4; ++si) {
-      unpack8c(dc[(size_t)si * total + t], u);
+      unpack8h<DT>(dc[(size_t)si * total + t], u);
 #pragma unroll
       for (int k = 0; k < 8; ++k) g[k] -= u[k];
     }
@@ -453,10 +445,10 @@ __global__ void __launch_bounds__(256) ctx_bwd_final_kernel(const uint4* __restr
       for (int k = 0; k < 8; ++k) g[k] += m * R.v[b][k];
     }
     float f[8];
-    unpack8c(fv[t], f);
+    unpack8h<DT>(fv[t], f);
 #pragma unroll
     for (int k = 0; k < 8; ++k) g[k] = (f[k] > 0.f) ? g[k] : 0.f;
-    dfv[t] = pack8c(g);
+    dfv[t] = pack8h<DT>(g);
   }
 }
 
@@ -470,19 +462,18 @@ static inline int gridn(size_t n, int cap = 8192) {
 
 using namespace can;
 
-// mode 0: POOL(fv -> ave cells); mode 1: BILINEAR^T(sdir+dc -> dA cells)
-extern "C" int can_ctx_reduce(int mode, const void* in0, const void* sdir, const void* dc, float* rowacc, float* cells,
-                              int N, int h, int w, int C, void* stream) {
-  if (C & 7) return -2;
-  hipStream_t s = (hipStream_t)stream;
-  if (w > 2048) return -3;                       // LDS bin-weight table [12][w]
+// mode 0: POOL(fv -> ave cells); mode 1: BILINEAR^T(sdir+dc -> dA cells).  dt: element type of the
+// 16-bit inputs (DT_BF16 = 0, DT_F16 = 1); rowacc / cells are fp32.
+template <int DT>
+static int ctx_reduce_impl(int mode, const void* in0, const void* sdir, const void* dc, float* rowacc, float* cells,
+                           int N, int h, int w, int C, hipStream_t s) {
   const int nb = N * h * ((C / 8 + 63) / 64);
   const size_t lds = (size_t)12 * w * sizeof(float);
   if (mode == 0)
-    hipLaunchKernelGGL(ctx_rows_kernel<true>, dim3(nb), dim3(256), lds, s, (const uint4*)in0, nullptr, nullptr,
+    hipLaunchKernelGGL((ctx_rows_kernel<DT, true>), dim3(nb), dim3(256), lds, s, (const uint4*)in0, nullptr, nullptr,
                        rowacc, N, h, w, C);
   else
-    hipLaunchKernelGGL(ctx_rows_kernel<false>, dim3(nb), dim3(256), lds, s, nullptr, (const uint4*)sdir,
+    hipLaunchKernelGGL((ctx_rows_kernel<DT, false>), dim3(nb), dim3(256), lds, s, nullptr, (const uint4*)sdir,
                        (const uint4*)dc, rowacc, N, h, w, C);
   const size_t tc = (size_t)N * 50 * C;
   if (mode == 0)
@@ -492,34 +483,43 @@ extern "C" int can_ctx_reduce(int mode, const void* in0, const void* sdir, const
   return (int)hipGetLastError();
 }
 
-extern "C" int can_ctx_expand(const void* fv, const float* T, void* cs, int N, int h, int w, int C, void* stream) {
+extern "C" int can_ctx_reduce(int mode, const void* in0, const void* sdir, const void* dc, float* rowacc, float* cells,
+                              int N, int h, int w, int C, int dt, void* stream) {
   if (C & 7) return -2;
-  hipLaunchKernelGGL(ctx_expand_kernel, dim3(N * h * ((C / 8 + 63) / 64) * 2), dim3(256), 0, (hipStream_t)stream,
-                     (const uint4*)fv, T, (uint4*)cs, N, h, w, C);
+  if (w > 2048) return -3;                       // LDS bin-weight table [12][w]
+  CAN_DT_DISPATCH(dt, ctx_reduce_impl<DT>(mode, in0, sdir, dc, rowacc, cells, N, h, w, C, (hipStream_t)stream));
+}
+
+static inline dim3 ctx_grid(int N, int h, int C) { return dim3(N * h * ((C / 8 + 63) / 64) * 2); }
+
+extern "C" int can_ctx_expand(const void* fv, const float* T, void* cs, int N, int h, int w, int C, int dt,
+                              void* stream) {
+  if (C & 7) return -2;
+  CAN_LAUNCH_DT(dt, ctx_expand_kernel, ctx_grid(N, h, C), dim3(256), 0, (hipStream_t)stream, (const uint4*)fv, T,
+                (uint4*)cs, N, h, w, C);
   return (int)hipGetLastError();
 }
 
 extern "C" int can_ctx_fuse(const void* fv, const void* ws, const float* T, void* cat, int N, int h, int w, int C,
-                            void* stream) {
+                            int dt, void* stream) {
   if (C & 7) return -2;
-  hipLaunchKernelGGL(ctx_fuse_kernel, dim3(N * h * ((C / 8 + 63) / 64) * 2), dim3(256), 0, (hipStream_t)stream,
-                     (const uint4*)fv, (const uint4*)ws, T, (uint4*)cat, N, h, w, C);
+  CAN_LAUNCH_DT(dt, ctx_fuse_kernel, ctx_grid(N, h, C), dim3(256), 0, (hipStream_t)stream, (const uint4*)fv,
+                (const uint4*)ws, T, (uint4*)cat, N, h, w, C);
   return (int)hipGetLastError();
 }
 
 extern "C" int can_ctx_bwd_e1(const void* dcat, const void* ws, const float* T, void* dz, void* sdir, int N, int h,
-                              int w, int C, void* stream) {
+                              int w, int C, int dt, void* stream) {
   if (C & 7) return -2;
-  hipLaunchKernelGGL(ctx_bwd_e1_kernel, dim3(N * h * ((C / 8 + 63) / 64) * 2), dim3(256), 0, (hipStream_t)stream,
-                     (const uint4*)dcat, (const uint4*)ws, T, (uint4*)dz, (uint4*)sdir, N, h, w, C);
+  CAN_LAUNCH_DT(dt, ctx_bwd_e1_kernel, ctx_grid(N, h, C), dim3(256), 0, (hipStream_t)stream, (const uint4*)dcat,
+                (const uint4*)ws, T, (uint4*)dz, (uint4*)sdir, N, h, w, C);
   return (int)hipGetLastError();
 }
 
 extern "C" int can_ctx_bwd_final(const void* dcat, const void* dc, const float* dave, const void* fv, void* dfv,
-                                 int N, int h, int w, int C, void* stream) {
+                                 int N, int h, int w, int C, int dt, void* stream) {
   if (C & 7) return -2;
-  hipLaunchKernelGGL(ctx_bwd_final_kernel, dim3(N * h * ((C / 8 + 63) / 64) * 2), dim3(256), 0,
-                     (hipStream_t)stream, (const uint4*)dcat, (const uint4*)dc, dave, (const uint4*)fv, (uint4*)dfv, N,
-                     h, w, C);
+  CAN_LAUNCH_DT(dt, ctx_bwd_final_kernel, ctx_grid(N, h, C), dim3(256), 0, (hipStream_t)stream, (const uint4*)dcat,
+                (const uint4*)dc, dave, (const uint4*)fv, (uint4*)dfv, N, h, w, C);
   return (int)hipGetLastError();
 }

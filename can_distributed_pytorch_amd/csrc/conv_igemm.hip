@@ -34,7 +34,6 @@
 
 namespace can {
 
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 
 struct ConvArgs {
   const bf16_t* x;     // NHWC [N][H][W][Cin] bf16 (FIRST: Cin = 4, channel 3 zero)
@@ -57,7 +56,7 @@ __device__ __forceinline__ int perm_row(int rho) {
 
 __device__ __forceinline__ int swz(int row, int chunk) { return (chunk ^ (row & 7)); }
 
-template <int WC, int WP, int LOAD, int EPI>
+template <int DT, int WC, int WP, int LOAD, int EPI>
 __global__ void __launch_bounds__(64 * WC * WP)
 conv_igemm_kernel(ConvArgs a) {
   constexpr int NT = 64 * WC * WP;
@@ -179,22 +178,22 @@ conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int chunk = kk * 4 + fq;
-      bf16x8_t af[4], bfr[4];
+      frag8_t af[4], bfr[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int row = wc * 64 + j * 16 + fr;
-        af[j] = __builtin_bit_cast(bf16x8_t, As[(buf * TC + row) * 8 + swz(row, chunk)]);
+        af[j] = __builtin_bit_cast(frag8_t, As[(buf * TC + row) * 8 + swz(row, chunk)]);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = wp * 64 + i * 16 + fr;
-        bfr[i] = __builtin_bit_cast(bf16x8_t, Bs[(buf * TP + row) * 8 + swz(row, chunk)]);
+        bfr[i] = __builtin_bit_cast(frag8_t, Bs[(buf * TP + row) * 8 + swz(row, chunk)]);
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], bfr[i], acc[j][i], 0, 0, 0);
+          acc[j][i] = mfma16<DT>(af[j], bfr[i], acc[j][i]);
     }
     if (ks + 1 < nk) store_stage(buf ^ 1);
     __syncthreads();
@@ -238,23 +237,23 @@ conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         const unsigned short bits = (unsigned short)(mw[c >> 1] >> ((c & 1) * 16));
-        const bool pos = ((bits & 0x8000u) == 0) && ((bits & 0x7fffu) != 0);
+        const bool pos = pos_bits(bits);
         v[c] = pos ? v[c] : 0.f;
       }
     }
-    uint4 o0 = make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
-    uint4 o1 = make_uint4(pack2bf(v[8], v[9]), pack2bf(v[10], v[11]), pack2bf(v[12], v[13]), pack2bf(v[14], v[15]));
+    uint4 o0 = make_uint4(pack2<DT>(v[0], v[1]), pack2<DT>(v[2], v[3]), pack2<DT>(v[4], v[5]), pack2<DT>(v[6], v[7]));
+    uint4 o1 = make_uint4(pack2<DT>(v[8], v[9]), pack2<DT>(v[10], v[11]), pack2<DT>(v[12], v[13]), pack2<DT>(v[14], v[15]));
     *reinterpret_cast<uint4*>(a.y + off) = o0;
     *reinterpret_cast<uint4*>(a.y + off + 8) = o1;
   }
 }
 
-template <int WC, int WP, int LOAD, int EPI>
+template <int DT, int WC, int WP, int LOAD, int EPI>
 static int launch_conv(const ConvArgs& a, hipStream_t s) {
   constexpr int NT = 64 * WC * WP;
   constexpr int TC = 64 * WC, TP = 64 * WP;
   const size_t lds = 2 * (TC + TP) * 128;
-  auto kfn = conv_igemm_kernel<WC, WP, LOAD, EPI>;
+  auto kfn = conv_igemm_kernel<DT, WC, WP, LOAD, EPI>;
   static bool attr_set = false;
   if (!attr_set) {
     CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -266,7 +265,7 @@ static int launch_conv(const ConvArgs& a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-template <int LOAD, int EPI>
+template <int DT, int LOAD, int EPI>
 static int dispatch_tiles(const ConvArgs& a, int tile_cfg, hipStream_t s) {
   // tile_cfg: 0 = auto, 1 = 128ch x 128pix, 2 = 64ch x 256pix, 3 = 128ch x 256pix, 4 = 256ch x 128pix
   int cfg = tile_cfg;
@@ -276,10 +275,10 @@ static int dispatch_tiles(const ConvArgs& a, int tile_cfg, hipStream_t s) {
     else cfg = 1;
   }
   switch (cfg) {
-    case 1: return launch_conv<2, 2, LOAD, EPI>(a, s);
-    case 2: return launch_conv<1, 4, LOAD, EPI>(a, s);
-    case 3: return launch_conv<2, 4, LOAD, EPI>(a, s);
-    case 4: return launch_conv<4, 2, LOAD, EPI>(a, s);
+    case 1: return launch_conv<DT, 2, 2, LOAD, EPI>(a, s);
+    case 2: return launch_conv<DT, 1, 4, LOAD, EPI>(a, s);
+    case 3: return launch_conv<DT, 2, 4, LOAD, EPI>(a, s);
+    case 4: return launch_conv<DT, 4, 2, LOAD, EPI>(a, s);
   }
   return -1;
 }
@@ -309,7 +308,7 @@ struct ConvArgs2 {
 
 // Shared epilogue of the LDS-DMA kernels: lane (fr, fq) of wave (wc, wp) owns
 // 16 consecutive output channels of one pixel per 16x16 pixel fragment.
-template <int WC, int WP, int PW, int EPI>
+template <int DT, int WC, int WP, int PW, int EPI>
 __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4][4 * PW], int ct, int pt,
                                               int wc, int wp, int fr, int fq) {
   constexpr int TC = 64 * WC, TP = 64 * PW * WP;
@@ -350,18 +349,18 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         const unsigned short bits = (unsigned short)(mw[c >> 1] >> ((c & 1) * 16));
-        const bool pos = ((bits & 0x8000u) == 0) && ((bits & 0x7fffu) != 0);
+        const bool pos = pos_bits(bits);
         v[c] = pos ? v[c] : 0.f;
       }
     }
     *reinterpret_cast<uint4*>(a.y + off) =
-        make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
+        make_uint4(pack2<DT>(v[0], v[1]), pack2<DT>(v[2], v[3]), pack2<DT>(v[4], v[5]), pack2<DT>(v[6], v[7]));
     *reinterpret_cast<uint4*>(a.y + off + 8) =
-        make_uint4(pack2bf(v[8], v[9]), pack2bf(v[10], v[11]), pack2bf(v[12], v[13]), pack2bf(v[14], v[15]));
+        make_uint4(pack2<DT>(v[8], v[9]), pack2<DT>(v[10], v[11]), pack2<DT>(v[12], v[13]), pack2<DT>(v[14], v[15]));
   }
 }
 
-template <int WC, int WP, int PW, int EPI>
+template <int DT, int WC, int WP, int PW, int EPI>
 __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds_kernel(ConvArgs2 a) {
   constexpr int NW = WC * WP;
   constexpr int TC = 64 * WC, TP = 64 * PW * WP;
@@ -438,26 +437,26 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds_kernel(ConvArgs2 a)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int chunk = kk * 4 + fq;
-      bf16x8_t af[4], bfr[4 * PW];
+      frag8_t af[4], bfr[4 * PW];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int row = wc * 64 + j * 16 + fr;
-        af[j] = __builtin_bit_cast(bf16x8_t, As[row * 8 + swz(row, chunk)]);
+        af[j] = __builtin_bit_cast(frag8_t, As[row * 8 + swz(row, chunk)]);
       }
 #pragma unroll
       for (int i = 0; i < 4 * PW; ++i) {
         const int row = wp * 64 * PW + i * 16 + fr;
-        bfr[i] = __builtin_bit_cast(bf16x8_t, Bs[row * 8 + swz(row, chunk)]);
+        bfr[i] = __builtin_bit_cast(frag8_t, Bs[row * 8 + swz(row, chunk)]);
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int i = 0; i < 4 * PW; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], bfr[i], acc[j][i], 0, 0, 0);
+          acc[j][i] = mfma16<DT>(af[j], bfr[i], acc[j][i]);
     }
   }
 
-  glds_epilogue<WC, WP, PW, EPI>(a, acc, ct, pt, wc, wp, fr, fq);
+  glds_epilogue<DT, WC, WP, PW, EPI>(a, acc, ct, pt, wc, wp, fr, fq);
 }
 
 // ===========================================================================
@@ -474,7 +473,7 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds_kernel(ConvArgs2 a)
 //    second half's MFMAs run, so LDS read latency is never exposed at the
 //    head of an MFMA burst.
 // ===========================================================================
-template <int WC, int WP, int PW, int EPI>
+template <int DT, int WC, int WP, int PW, int EPI>
 __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a) {
   constexpr int NW = WC * WP;
   constexpr int TC = 64 * WC, TP = 64 * PW * WP;
@@ -562,31 +561,31 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
     for (int i = 0; i < 4 * PW; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fq = lane >> 4;
-  auto read = [&](int buf, int kk, bf16x8_t (&af)[4], bf16x8_t (&bfr)[4 * PW]) {
+  auto read = [&](int buf, int kk, frag8_t (&af)[4], frag8_t (&bfr)[4 * PW]) {
     const uint4* As = reinterpret_cast<const uint4*>(smem + buf * STAGE);
     const uint4* Bs = reinterpret_cast<const uint4*>(smem + buf * STAGE + A_BYTES);
     const int chunk = kk * 4 + fq;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int row = wc * 64 + j * 16 + fr;
-      af[j] = __builtin_bit_cast(bf16x8_t, As[row * 8 + swz(row, chunk)]);
+      af[j] = __builtin_bit_cast(frag8_t, As[row * 8 + swz(row, chunk)]);
     }
 #pragma unroll
     for (int i = 0; i < 4 * PW; ++i) {
       const int row = wp * 64 * PW + i * 16 + fr;
-      bfr[i] = __builtin_bit_cast(bf16x8_t, Bs[row * 8 + swz(row, chunk)]);
+      bfr[i] = __builtin_bit_cast(frag8_t, Bs[row * 8 + swz(row, chunk)]);
     }
   };
   // MFMAs over pixel fragments [i0, i1) (so the B fragments die in halves)
-  auto mma = [&](const bf16x8_t (&af)[4], const bf16x8_t (&bfr)[4 * PW], int i0, int i1) {
+  auto mma = [&](const frag8_t (&af)[4], const frag8_t (&bfr)[4 * PW], int i0, int i1) {
 #pragma unroll
     for (int i = i0; i < i1; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], bfr[i], acc[j][i], 0, 0, 0);
+        acc[j][i] = mfma16<DT>(af[j], bfr[i], acc[j][i]);
   };
 
-  bf16x8_t a0[4], b0[4 * PW], a1[4], b1[4 * PW];
+  frag8_t a0[4], b0[4 * PW], a1[4], b1[4 * PW];
   issue(0);
   if (nk > 1) {
     issue(1);
@@ -624,14 +623,14 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
   read((nk - 1) & 1, 1, a1, b1);
   mma(a0, b0, 0, 4 * PW);
   mma(a1, b1, 0, 4 * PW);
-  glds_epilogue<WC, WP, PW, EPI>(a, acc, ct, pt, wc, wp, fr, fq);
+  glds_epilogue<DT, WC, WP, PW, EPI>(a, acc, ct, pt, wc, wp, fr, fq);
 }
 
-template <int WC, int WP, int PW, int EPI>
+template <int DT, int WC, int WP, int PW, int EPI>
 static int launch_glds2(const ConvArgs2& a, hipStream_t s) {
   constexpr int TC = 64 * WC, TP = 64 * PW * WP;
   const size_t lds = 2 * (size_t)(TC + TP) * 128;
-  auto kfn = conv_glds2_kernel<WC, WP, PW, EPI>;
+  auto kfn = conv_glds2_kernel<DT, WC, WP, PW, EPI>;
   static bool attr = false;
   if (!attr) {
     CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -663,7 +662,7 @@ struct HaloConvArgs {
   int N, H, W, tiles_x, tiles_y;
 };
 
-template <int CO, int EPI>
+template <int DT, int CO, int EPI>
 __global__ void __launch_bounds__(512, 1) conv_halo64_kernel(HaloConvArgs a) {
   constexpr int TR = 4, TCOL = 128, HR = TR + 2, HC = TCOL + 2;
   constexpr int HPIX = HR * HC;                       // 780 halo pixels
@@ -743,19 +742,19 @@ __global__ void __launch_bounds__(512, 1) conv_halo64_kernel(HaloConvArgs a) {
     const unsigned char* Ab = wring + (t % 3) * WTAP;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8_t af[4], bfr[4 * PW];
+      frag8_t af[4], bfr[4 * PW];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        af[j] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(Ab + woff[kk] + j * 2048));
+        af[j] = __builtin_bit_cast(frag8_t, *reinterpret_cast<const uint4*>(Ab + woff[kk] + j * 2048));
 #pragma unroll
       for (int i = 0; i < 4 * PW; ++i)
-        bfr[i] = __builtin_bit_cast(bf16x8_t,
+        bfr[i] = __builtin_bit_cast(frag8_t,
                                     *reinterpret_cast<const uint4*>(halo + hoff[kw][kk] + kh * HC * 128 + i * 2048));
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int i = 0; i < 4 * PW; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], bfr[i], acc[j][i], 0, 0, 0);
+          acc[j][i] = mfma16<DT>(af[j], bfr[i], acc[j][i]);
     }
   }
 
@@ -795,14 +794,14 @@ __global__ void __launch_bounds__(512, 1) conv_halo64_kernel(HaloConvArgs a) {
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         const unsigned short bits = (unsigned short)(mw[c >> 1] >> ((c & 1) * 16));
-        const bool pos = ((bits & 0x8000u) == 0) && ((bits & 0x7fffu) != 0);
+        const bool pos = pos_bits(bits);
         v[c] = pos ? v[c] : 0.f;
       }
     }
     *reinterpret_cast<uint4*>(a.y + off) =
-        make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
+        make_uint4(pack2<DT>(v[0], v[1]), pack2<DT>(v[2], v[3]), pack2<DT>(v[4], v[5]), pack2<DT>(v[6], v[7]));
     *reinterpret_cast<uint4*>(a.y + off + 8) =
-        make_uint4(pack2bf(v[8], v[9]), pack2bf(v[10], v[11]), pack2bf(v[12], v[13]), pack2bf(v[14], v[15]));
+        make_uint4(pack2<DT>(v[8], v[9]), pack2<DT>(v[10], v[11]), pack2<DT>(v[12], v[13]), pack2<DT>(v[14], v[15]));
   }
 }
 
@@ -815,6 +814,7 @@ __global__ void __launch_bounds__(512, 1) conv_halo64_kernel(HaloConvArgs a) {
 // into registers; each B fragment is two ds_read_b64 (taps 2q, 2q+1 of one
 // pixel, 4 channels each); K = 64 = 2 MFMA k-steps (taps 9..15 are zero).
 // ===========================================================================
+template <int DT>
 __global__ void __launch_bounds__(512) conv_first_halo_kernel(HaloConvArgs a) {
   constexpr int TR = 4, TCOL = 128, HC = TCOL + 2, HPIX = (TR + 2) * HC;
   __shared__ uint2 halo[HPIX];
@@ -834,12 +834,12 @@ __global__ void __launch_bounds__(512) conv_first_halo_kernel(HaloConvArgs a) {
     halo[hp] = v;
   }
   const int fr = lane & 15, fq = lane >> 4;
-  bf16x8_t af[2][4];
+  frag8_t af[2][4];
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      af[kk][j] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(a.w + perm_row(j * 16 + fr) * 64 + kk * 32 + fq * 8));
+      af[kk][j] = __builtin_bit_cast(frag8_t, *reinterpret_cast<const uint4*>(a.w + perm_row(j * 16 + fr) * 64 + kk * 32 + fq * 8));
   __syncthreads();
 
   const int r = wave >> 1, colbase = (wave & 1) * 64;
@@ -851,7 +851,7 @@ __global__ void __launch_bounds__(512) conv_first_halo_kernel(HaloConvArgs a) {
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
     const int t0 = kk * 8 + fq * 2;                 // this lane's taps t0, t0+1
-    bf16x8_t bfr[4];
+    frag8_t bfr[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       uint2 lo = make_uint2(0u, 0u), hi = make_uint2(0u, 0u);
@@ -864,13 +864,13 @@ __global__ void __launch_bounds__(512) conv_first_halo_kernel(HaloConvArgs a) {
         const int kh = ((t0 + 1) * 11) >> 5, kw = t0 + 1 - kh * 3;
         hi = halo[(r + kh) * HC + c + kw];
       }
-      bfr[i] = __builtin_bit_cast(bf16x8_t, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      bfr[i] = __builtin_bit_cast(frag8_t, make_uint4(lo.x, lo.y, hi.x, hi.y));
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][j], bfr[i], acc[j][i], 0, 0, 0);
+        acc[j][i] = mfma16<DT>(af[kk][j], bfr[i], acc[j][i]);
   }
 
   const int oh = oh0 + r;
@@ -893,17 +893,17 @@ __global__ void __launch_bounds__(512) conv_first_halo_kernel(HaloConvArgs a) {
       for (int q = 0; q < 4; ++q) v[j * 4 + q] = fmaxf(acc[j][i][q] + bias[j * 4 + q], 0.f);
     const size_t off = ((size_t)(n * a.H + oh) * a.W + ow) * 64 + chb;
     *reinterpret_cast<uint4*>(a.y + off) =
-        make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
+        make_uint4(pack2<DT>(v[0], v[1]), pack2<DT>(v[2], v[3]), pack2<DT>(v[4], v[5]), pack2<DT>(v[6], v[7]));
     *reinterpret_cast<uint4*>(a.y + off + 8) =
-        make_uint4(pack2bf(v[8], v[9]), pack2bf(v[10], v[11]), pack2bf(v[12], v[13]), pack2bf(v[14], v[15]));
+        make_uint4(pack2<DT>(v[8], v[9]), pack2<DT>(v[10], v[11]), pack2<DT>(v[12], v[13]), pack2<DT>(v[14], v[15]));
   }
 }
 
-template <int CO, int EPI>
+template <int DT, int CO, int EPI>
 static int launch_halo64(const HaloConvArgs& a, hipStream_t s) {
   constexpr int HALO_BYTES = ((6 * 130 + 7) / 8) * 1024;
   const size_t lds = HALO_BYTES + 3 * (size_t)CO * 128;
-  auto kfn = conv_halo64_kernel<CO, EPI>;
+  auto kfn = conv_halo64_kernel<DT, CO, EPI>;
   static bool attr = false;
   if (!attr) {
     CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -913,11 +913,11 @@ static int launch_halo64(const HaloConvArgs& a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-template <int WC, int WP, int PW, int EPI>
+template <int DT, int WC, int WP, int PW, int EPI>
 static int launch_glds(const ConvArgs2& a, hipStream_t s) {
   constexpr int TC = 64 * WC, TP = 64 * PW * WP;
   const size_t lds = 2 * (size_t)(TC + TP) * 128;
-  auto kfn = conv_glds_kernel<WC, WP, PW, EPI>;
+  auto kfn = conv_glds_kernel<DT, WC, WP, PW, EPI>;
   static bool attr = false;
   if (!attr) {
     CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -928,7 +928,7 @@ static int launch_glds(const ConvArgs2& a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-template <int EPI>
+template <int DT, int EPI>
 static int dispatch_glds(const ConvArgs2& a, int tile_cfg, hipStream_t s) {
   int cfg = tile_cfg;
   if (cfg == 0) {   // v2 (pipelined) by default; 128 x 512 tiles measured faster for K <= 1152
@@ -936,13 +936,13 @@ static int dispatch_glds(const ConvArgs2& a, int tile_cfg, hipStream_t s) {
     cfg = (a.Cout % 256 == 0) ? 21 : (a.Cout % 128 == 0) ? (ktot <= 1152 ? 25 : 22) : 23;
   }
   switch (cfg) {
-    case 11: if (a.Cout % 256) return -8; return launch_glds<4, 2, 2, EPI>(a, s);
-    case 12: if (a.Cout % 128) return -8; return launch_glds<2, 4, 1, EPI>(a, s);
-    case 13: return launch_glds<1, 8, 1, EPI>(a, s);
-    case 21: if (a.Cout % 256) return -8; return launch_glds2<4, 2, 2, EPI>(a, s);
-    case 22: if (a.Cout % 128) return -8; return launch_glds2<2, 4, 1, EPI>(a, s);
-    case 23: return launch_glds2<1, 8, 1, EPI>(a, s);
-    case 25: if (a.Cout % 128) return -8; return launch_glds2<2, 4, 2, EPI>(a, s);   // 128 x 512, 160 KB LDS
+    case 11: if (a.Cout % 256) return -8; return launch_glds<DT, 4, 2, 2, EPI>(a, s);
+    case 12: if (a.Cout % 128) return -8; return launch_glds<DT, 2, 4, 1, EPI>(a, s);
+    case 13: return launch_glds<DT, 1, 8, 1, EPI>(a, s);
+    case 21: if (a.Cout % 256) return -8; return launch_glds2<DT, 4, 2, 2, EPI>(a, s);
+    case 22: if (a.Cout % 128) return -8; return launch_glds2<DT, 2, 4, 1, EPI>(a, s);
+    case 23: return launch_glds2<DT, 1, 8, 1, EPI>(a, s);
+    case 25: if (a.Cout % 128) return -8; return launch_glds2<DT, 2, 4, 2, EPI>(a, s);   // 128 x 512, 160 KB LDS
   }
   return -9;
 }
@@ -956,12 +956,10 @@ static const bf16_t* conv_zero_page() {
   return (const bf16_t*)z;
 }
 
-}  // namespace can
-
-extern "C" int can_conv_igemm(const void* x, const void* w, const float* bias, const void* mask, void* y,
-                              int N, int H, int W, int Cin, int Cout, int ksize, int dil,
-                              int epi, int first, int tile_cfg, void* stream) {
-  using namespace can;
+template <int DT>
+static int conv_igemm_impl(const void* x, const void* w, const float* bias, const void* mask, void* y,
+                           int N, int H, int W, int Cin, int Cout, int ksize, int dil,
+                           int epi, int first, int tile_cfg, void* stream) {
   ConvArgs a;
   a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.bias = bias; a.mask = (const bf16_t*)mask;
   a.y = (bf16_t*)y; a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.ksize = ksize; a.dil = dil;
@@ -971,14 +969,14 @@ extern "C" int can_conv_igemm(const void* x, const void* w, const float* bias, c
   if (first && (Cin != 4 || ksize != 3)) return -4;
   hipStream_t s = (hipStream_t)stream;
 #define CAN_EPI_CASE(L, E) \
-  if (epi == E) return dispatch_tiles<L, E>(a, tile_cfg, s);
+  if (epi == E) return dispatch_tiles<DT, L, E>(a, tile_cfg, s);
   const bool auto_halo = tile_cfg == 0 && getenv("CANNET_NO_HALO_CONV") == nullptr;
   if (first) {
     if ((tile_cfg == 32 || auto_halo) && Cout == 64 && epi == EPI_BIAS_RELU) {
       HaloConvArgs h;
       h.x = a.x; h.w = a.w; h.bias = a.bias; h.mask = nullptr; h.y = a.y; h.zero = nullptr;
       h.N = N; h.H = H; h.W = W; h.tiles_x = (W + 127) / 128; h.tiles_y = (H + 3) / 4;
-      hipLaunchKernelGGL(conv_first_halo_kernel, dim3(N * h.tiles_y * h.tiles_x), dim3(512), 0, s, h);
+      hipLaunchKernelGGL(conv_first_halo_kernel<DT>, dim3(N * h.tiles_y * h.tiles_x), dim3(512), 0, s, h);
       return (int)hipGetLastError();
     }
     CAN_EPI_CASE(LOAD_FIRST, EPI_BIAS_RELU)
@@ -994,7 +992,7 @@ extern "C" int can_conv_igemm(const void* x, const void* w, const float* bias, c
     if (!h.zero) return -10;
     h.N = N; h.H = H; h.W = W; h.tiles_x = (W + 127) / 128; h.tiles_y = (H + 3) / 4;
 #define CAN_HALO_CASE(E) \
-    if (epi == E) return (Cout == 64) ? launch_halo64<64, E>(h, s) : launch_halo64<128, E>(h, s);
+    if (epi == E) return (Cout == 64) ? launch_halo64<DT, 64, E>(h, s) : launch_halo64<DT, 128, E>(h, s);
     CAN_HALO_CASE(EPI_BIAS_RELU)
     CAN_HALO_CASE(EPI_MASK)
     CAN_HALO_CASE(EPI_NONE)
@@ -1010,11 +1008,11 @@ extern "C" int can_conv_igemm(const void* x, const void* w, const float* bias, c
     b.H = H; b.W = W; b.Cin = Cin; b.Cout = Cout; b.ksize = ksize; b.dil = dil; b.M = a.M;
     b.fdW = make_fastdiv((uint32_t)W); b.fdH = make_fastdiv((uint32_t)H);
     switch (epi) {
-      case EPI_BIAS_RELU: return dispatch_glds<EPI_BIAS_RELU>(b, tile_cfg, s);
-      case EPI_MASK: return dispatch_glds<EPI_MASK>(b, tile_cfg, s);
-      case EPI_NONE: return dispatch_glds<EPI_NONE>(b, tile_cfg, s);
-      case EPI_BIAS: return dispatch_glds<EPI_BIAS>(b, tile_cfg, s);
-      case EPI_SIGMOID: return dispatch_glds<EPI_SIGMOID>(b, tile_cfg, s);
+      case EPI_BIAS_RELU: return dispatch_glds<DT, EPI_BIAS_RELU>(b, tile_cfg, s);
+      case EPI_MASK: return dispatch_glds<DT, EPI_MASK>(b, tile_cfg, s);
+      case EPI_NONE: return dispatch_glds<DT, EPI_NONE>(b, tile_cfg, s);
+      case EPI_BIAS: return dispatch_glds<DT, EPI_BIAS>(b, tile_cfg, s);
+      case EPI_SIGMOID: return dispatch_glds<DT, EPI_SIGMOID>(b, tile_cfg, s);
     }
     return -6;
   }
@@ -1025,4 +1023,14 @@ extern "C" int can_conv_igemm(const void* x, const void* w, const float* bias, c
   CAN_EPI_CASE(LOAD_GENERIC, EPI_SIGMOID)
 #undef CAN_EPI_CASE
   return -6;
+}
+
+}  // namespace can
+
+// dt: element type of x / w / mask / y (DT_BF16 = 0, DT_F16 = 1)
+extern "C" int can_conv_igemm(const void* x, const void* w, const float* bias, const void* mask, void* y,
+                              int N, int H, int W, int Cin, int Cout, int ksize, int dil,
+                              int epi, int first, int tile_cfg, int dt, void* stream) {
+  CAN_DT_DISPATCH(dt, can::conv_igemm_impl<DT>(x, w, bias, mask, y, N, H, W, Cin, Cout, ksize, dil, epi, first,
+                                              tile_cfg, stream));
 }

@@ -34,7 +34,6 @@
 
 namespace can {
 
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
@@ -54,7 +53,7 @@ __device__ __forceinline__ int swz8(int row, int c8) {
   else return c8 ^ (((((row >> 1) & 1)) | (((row >> 3) & 1) << 1)) << 2);
 }
 
-template <int WC, int WK, int WM, bool FIRST>
+template <int DT, int WC, int WK, int WM, bool FIRST>
 __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
   constexpr int TCo = 64 * WC;
   constexpr int TK = 64 * WK;
@@ -167,13 +166,11 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  bf16x8_t ones;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+  const frag8_t ones = ones_frag<DT>();
 
   // transposed fragment read: 8 consecutive pixels (rows) of one column
   const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
-  auto read_frag = [&](const bf16_t* base, int rw_is128, int prow0, int col0) -> bf16x8_t {
+  auto read_frag = [&](const bf16_t* base, int rw_is128, int prow0, int col0) -> frag8_t {
     s16x4 lo, hi;
     const int r0 = prow0 + 8 * g + q;
     const int c8 = (col0 >> 2) + p;
@@ -186,7 +183,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
     }
     typedef short s16x8 __attribute__((ext_vector_type(8)));
     s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8_t, v);
+    return __builtin_bit_cast(frag8_t, v);
   };
 
   if (nstage > 0) {
@@ -202,7 +199,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
 #pragma unroll
     for (int kk = 0; kk < KSUB; ++kk) {
       const int prow0 = wm * (32 * KSUB) + kk * 32;
-      bf16x8_t af[4], bfr[4];
+      frag8_t af[4], bfr[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) af[j] = read_frag(Ab, TCo == 128, prow0, wc * 64 + j * 16);
 #pragma unroll
@@ -211,13 +208,13 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], bfr[i], acc[j][i], 0, 0, 0);
+          acc[j][i] = mfma16<DT>(af[j], bfr[i], acc[j][i]);
       // bias gradient: sum over pixels = MFMA against a ones operand.  Static
       // indices only (a runtime-indexed accumulator array spills to VGPR copies).
       if (do_bias && (WM != 1 || wk == 0)) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          accb[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], ones, accb[j], 0, 0, 0);
+          accb[j] = mfma16<DT>(af[j], ones, accb[j]);
       }
     }
     if (st + 1 < nstage) store_stage(buf ^ 1);
@@ -303,6 +300,10 @@ struct WgradArgs2 {
   float* wsb;
   int H, W, Cin, Cout, ksize, dil, M, K, S, mslice;
   FastDiv fdW, fdH, fdC;
+  // batched GEMMs (wgrad_glds2 only): nb independent problems of the same shape,
+  // operands nb apart by these element strides, slabs by S*K*Cout (default 1 / 0)
+  int nb = 1;
+  long long dy_bs = 0, x_bs = 0;
 };
 
 template <int RB>   // row bytes
@@ -311,7 +312,7 @@ __device__ __forceinline__ int swz8b(int row, int c8) {
   else return c8 ^ (((((row >> 1) & 1)) | (((row >> 3) & 1) << 1)) << 2);
 }
 
-template <int WC, int WK, int WM, int NBUF, int KW, int KK>
+template <int DT, int WC, int WK, int WM, int NBUF, int KW, int KK>
 __global__ void __launch_bounds__(64 * WC * WK * WM, (WC * WK * WM >= 8) ? 1 : 2) wgrad_glds_kernel(WgradArgs2 a) {
   constexpr int NW = WC * WK * WM;
   constexpr int TCo = 64 * WC, TK = 64 * WK * KW;
@@ -398,12 +399,10 @@ __global__ void __launch_bounds__(64 * WC * WK * WM, (WC * WK * WM >= 8) ? 1 : 2
 #pragma unroll
     for (int i = 0; i < 4 * KW; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  bf16x8_t ones;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+  const frag8_t ones = ones_frag<DT>();
 
   const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
-  auto rd = [&](const unsigned char* base, int rb_is_wide, int rb, int prow0, int col0) -> bf16x8_t {
+  auto rd = [&](const unsigned char* base, int rb_is_wide, int rb, int prow0, int col0) -> frag8_t {
     const int r0 = prow0 + 8 * g + q;
     const int c8 = (col0 >> 2) + p;
     const int s0 = rb_is_wide ? swz8b<256>(r0, c8) : swz8b<128>(r0, c8);
@@ -412,7 +411,7 @@ __global__ void __launch_bounds__(64 * WC * WK * WM, (WC * WK * WM >= 8) ? 1 : 2
     const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + (r0 + 4) * rb + s1 * 8));
     typedef short s16x8 __attribute__((ext_vector_type(8)));
     const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8_t, v);
+    return __builtin_bit_cast(frag8_t, v);
   };
 
   // prologue: D stages in flight
@@ -434,7 +433,7 @@ __global__ void __launch_bounds__(64 * WC * WK * WM, (WC * WK * WM >= 8) ? 1 : 2
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
       const int prow0 = wm * 32 * KK + kk * 32;
-      bf16x8_t af[4], bfr[4 * KW];
+      frag8_t af[4], bfr[4 * KW];
 #pragma unroll
       for (int j = 0; j < 4; ++j) af[j] = rd(Ab, RBA >= 256, RBA, prow0, wc * 64 + j * 16);
 #pragma unroll
@@ -443,10 +442,10 @@ __global__ void __launch_bounds__(64 * WC * WK * WM, (WC * WK * WM >= 8) ? 1 : 2
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int i = 0; i < 4 * KW; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], bfr[i], acc[j][i], 0, 0, 0);
+          acc[j][i] = mfma16<DT>(af[j], bfr[i], acc[j][i]);
       if (do_bias && wk == 0) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) accb[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], ones, accb[j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j) accb[j] = mfma16<DT>(af[j], ones, accb[j]);
       }
     }
   }
@@ -518,13 +517,13 @@ __global__ void __launch_bounds__(64 * WC * WK * WM, (WC * WK * WM >= 8) ? 1 : 2
   }
 }
 
-template <int WC, int WK, int WM, int NBUF, int KW, int KK>
+template <int DT, int WC, int WK, int WM, int NBUF, int KW, int KK>
 static int launch_wgrad2(const WgradArgs2& a, hipStream_t s) {
   constexpr int NW = WC * WK * WM;
   constexpr int STAGE = 32 * KK * WM * (64 * WC + 64 * WK * KW) * 2;
   size_t lds = (size_t)NBUF * STAGE;
   if (WM > 1) lds = std::max(lds, (size_t)(NW * 16 * 64 * 4 + NW * 4 * 64 * 4) * 4);
-  auto kfn = wgrad_glds_kernel<WC, WK, WM, NBUF, KW, KK>;
+  auto kfn = wgrad_glds_kernel<DT, WC, WK, WM, NBUF, KW, KK>;
   static bool attr = false;
   if (!attr) {
     CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -547,7 +546,7 @@ static int launch_wgrad2(const WgradArgs2& a, hipStream_t s) {
 // first half's MFMAs, the next stage's first half read right after the
 // barrier under the other half).
 // ===========================================================================
-template <int WC, int WK, int KW>
+template <int DT, int WC, int WK, int KW>
 __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2 a) {
   constexpr int NW = WC * WK;
   constexpr int TCo = 64 * WC, TK = 64 * WK * KW;
@@ -567,16 +566,18 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
 
   const int nco = a.Cout / TCo, nkt = a.K / TK;
   const int ntile = nco * nkt;
-  const int bid = xcd_remap(blockIdx.x, ntile * a.S);
-  const int tile = bid % ntile, slice = bid / ntile;
+  const int bid = xcd_remap(blockIdx.x, ntile * a.S * a.nb);
+  const int tile = bid % ntile, slice = (bid / ntile) % a.S, bt = bid / (ntile * a.S);
   const int co0 = (tile % nco) * TCo, k0 = (tile / nco) * TK;
   const int mbeg = slice * a.mslice;
   const int mend = min(a.M, mbeg + a.mslice);
   const int nstage = (mend > mbeg) ? (mend - mbeg) / BKM : 0;   // M, mslice multiples of 64
+  const bf16_t* gdy = a.dy + bt * a.dy_bs;
+  const bf16_t* gx = a.x + bt * a.x_bs;
 
   // dY tile through a buffer resource: per-lane 32-bit offsets, stage base in soffset
   const __amdgpu_buffer_rsrc_t dy_rsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, (short)0, a.M * a.Cout * 2, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)gdy, (short)0, a.M * a.Cout * 2, 0x00020000);
   unsigned aoff[GA];
 #pragma unroll
   for (int j = 0; j < GA; ++j) {
@@ -616,7 +617,7 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
     for (int j = 0; j < GA; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(dy_rsrc, (__attribute__((address_space(3))) void*)(sbase + (wave + NW * j) * 1024),
                                                16, (int)aoff[j], (int)soff, 0, 0);
-    const bf16_t* xs = a.x + (size_t)m0 * a.Cin;
+    const bf16_t* xs = gx + (size_t)m0 * a.Cin;
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
       const int iw = ow0 + dw + 2 * (wave + NW * j) + lrow;
@@ -633,7 +634,7 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
     for (int i = 0; i < 4 * KW; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int g = lane >> 4, qd = (lane & 15) >> 2, p = lane & 3;
-  auto rd = [&](const unsigned char* base, int rb_wide, int rb, int prow0, int col0) -> bf16x8_t {
+  auto rd = [&](const unsigned char* base, int rb_wide, int rb, int prow0, int col0) -> frag8_t {
     const int r0 = prow0 + 8 * g + qd;
     const int c8 = (col0 >> 2) + p;
     const int s0 = rb_wide ? swz8b<256>(r0, c8) : swz8b<128>(r0, c8);
@@ -642,9 +643,9 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
     const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + (r0 + 4) * rb + s1 * 8));
     typedef short s16x8 __attribute__((ext_vector_type(8)));
     const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8_t, v);
+    return __builtin_bit_cast(frag8_t, v);
   };
-  auto read = [&](int buf, int kk, bf16x8_t (&af)[4], bf16x8_t (&bfr)[4 * KW]) {
+  auto read = [&](int buf, int kk, frag8_t (&af)[4], frag8_t (&bfr)[4 * KW]) {
     const unsigned char* Ab = smem + buf * STAGE;
     const unsigned char* Bb = Ab + A_BYTES;
     const int prow0 = kk * 32;
@@ -653,16 +654,16 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
 #pragma unroll
     for (int i = 0; i < 4 * KW; ++i) bfr[i] = rd(Bb, RBB >= 256, RBB, prow0, wk * 64 * KW + i * 16);
   };
-  auto mma = [&](const bf16x8_t (&af)[4], const bf16x8_t (&bfr)[4 * KW], int i0, int i1) {
+  auto mma = [&](const frag8_t (&af)[4], const frag8_t (&bfr)[4 * KW], int i0, int i1) {
 #pragma unroll
     for (int i = i0; i < i1; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], bfr[i], acc[j][i], 0, 0, 0);
+        acc[j][i] = mfma16<DT>(af[j], bfr[i], acc[j][i]);
   };
 
   if (nstage > 0) {
-    bf16x8_t a0[4], b0[4 * KW], a1[4], b1[4 * KW];
+    frag8_t a0[4], b0[4 * KW], a1[4], b1[4 * KW];
     issue(0, 0);
     if (nstage > 1) {
       issue(1, 1);
@@ -697,7 +698,7 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
   }
 
   const int fr = lane & 15, fq = lane >> 4;
-  float* slab = a.ws + (size_t)slice * a.K * a.Cout;
+  float* slab = a.ws + ((size_t)bt * a.S + slice) * a.K * a.Cout;
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -711,6 +712,7 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
 // Bias gradient partials for the v2 path: part[b][co] = sum of dY rows of
 // chunk b (SB chunks, fixed order; wgrad_reduce sums the SB partials).  A
 // separate short launch with many blocks, so the GEMM grid stays whole rounds.
+template <int DT>
 __global__ void __launch_bounds__(256) bias_colsum_kernel(const bf16_t* __restrict__ dy, float* __restrict__ part,
                                                           int M, int Cout, int SB) {
   __shared__ float red[256 * 8];
@@ -732,8 +734,8 @@ __global__ void __launch_bounds__(256) bias_colsum_kernel(const bf16_t* __restri
         const unsigned w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
         for (int e2 = 0; e2 < 4; ++e2) {
-          s[2 * e2] += __uint_as_float(w4[e2] << 16);
-          s[2 * e2 + 1] += __uint_as_float(w4[e2] & 0xffff0000u);
+          s[2 * e2] += h2f<DT>((unsigned short)(w4[e2] & 0xffffu));
+          s[2 * e2 + 1] += h2f<DT>((unsigned short)(w4[e2] >> 16));
         }
       }
     }
@@ -742,8 +744,8 @@ __global__ void __launch_bounds__(256) bias_colsum_kernel(const bf16_t* __restri
       const unsigned w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int e2 = 0; e2 < 4; ++e2) {
-        s[2 * e2] += __uint_as_float(w4[e2] << 16);
-        s[2 * e2 + 1] += __uint_as_float(w4[e2] & 0xffff0000u);
+        s[2 * e2] += h2f<DT>((unsigned short)(w4[e2] & 0xffffu));
+        s[2 * e2 + 1] += h2f<DT>((unsigned short)(w4[e2] >> 16));
       }
     }
   }
@@ -760,18 +762,18 @@ __global__ void __launch_bounds__(256) bias_colsum_kernel(const bf16_t* __restri
   }
 }
 
-template <int WC, int WK, int KW>
+template <int DT, int WC, int WK, int KW>
 static int launch_wgrad3(const WgradArgs2& a, hipStream_t s) {
   constexpr int STAGE = 64 * (64 * WC + 64 * WK * KW) * 2;
   const size_t lds = 2 * (size_t)STAGE;
-  auto kfn = wgrad_glds2_kernel<WC, WK, KW>;
+  auto kfn = wgrad_glds2_kernel<DT, WC, WK, KW>;
   static bool attr = false;
   if (!attr) {
     CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
   const int ntile = (a.Cout / (64 * WC)) * (a.K / (64 * WK * KW));
-  hipLaunchKernelGGL(kfn, dim3(ntile * a.S), dim3(64 * WC * WK), lds, s, a);
+  hipLaunchKernelGGL(kfn, dim3(ntile * a.S * a.nb), dim3(64 * WC * WK), lds, s, a);
   return (int)hipGetLastError();
 }
 
@@ -798,7 +800,7 @@ struct HaloArgs {
   int tiles_y, tiles_x, ntiles, tiles_per_slice;
 };
 
-template <int CO, int TH>
+template <int DT, int CO, int TH>
 __global__ void __launch_bounds__(576, 1) wgrad_halo_kernel(HaloArgs a) {
   constexpr int TW = 64;
   constexpr int HW_ = TW + 2;                       // halo width
@@ -863,12 +865,10 @@ __global__ void __launch_bounds__(576, 1) wgrad_halo_kernel(HaloArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  bf16x8_t ones;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+  const frag8_t ones = ones_frag<DT>();
   const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
   // transposed read of 8 consecutive rows r0.. (pixels) at column col0 of an LDS image with RB-byte rows
-  auto rd = [&](const unsigned char* base, auto rbc, int prow0, int col0) -> bf16x8_t {
+  auto rd = [&](const unsigned char* base, auto rbc, int prow0, int col0) -> frag8_t {
     constexpr int RB = decltype(rbc)::value;
     const int r0 = prow0 + 8 * g + q;
     const int c8 = (col0 >> 2) + p;
@@ -877,7 +877,7 @@ __global__ void __launch_bounds__(576, 1) wgrad_halo_kernel(HaloArgs a) {
         __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + (r0 + 4) * RB + swz8b<RB>(r0 + 4, c8) * 8));
     typedef short s16x8 __attribute__((ext_vector_type(8)));
     const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8_t, v);
+    return __builtin_bit_cast(frag8_t, v);
   };
   using RBdy = std::integral_constant<int, RBD>;
   using RBx = std::integral_constant<int, 128>;
@@ -894,7 +894,7 @@ __global__ void __launch_bounds__(576, 1) wgrad_halo_kernel(HaloArgs a) {
       for (int gg = 0; gg < TW / 32; ++gg) {
         const int prow_d = r * TW + gg * 32;
         const int prow_x = (r + kh) * HW_ + gg * 32 + kw;
-        bf16x8_t af[NT], bfr[4];
+        frag8_t af[NT], bfr[4];
 #pragma unroll
         for (int j = 0; j < NT; ++j) af[j] = rd(Db, RBdy{}, prow_d, j * 16);
 #pragma unroll
@@ -903,10 +903,10 @@ __global__ void __launch_bounds__(576, 1) wgrad_halo_kernel(HaloArgs a) {
         for (int j = 0; j < NT; ++j)
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], bfr[i], acc[j][i], 0, 0, 0);
+            acc[j][i] = mfma16<DT>(af[j], bfr[i], acc[j][i]);
         if (do_bias) {
 #pragma unroll
-          for (int j = 0; j < NT; ++j) accb[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], ones, accb[j], 0, 0, 0);
+          for (int j = 0; j < NT; ++j) accb[j] = mfma16<DT>(af[j], ones, accb[j]);
         }
       }
     }
@@ -929,13 +929,13 @@ __global__ void __launch_bounds__(576, 1) wgrad_halo_kernel(HaloArgs a) {
   }
 }
 
-template <int CO, int TH>
+template <int DT, int CO, int TH>
 static int launch_halo(HaloArgs& a, hipStream_t s) {
   constexpr int TW = 64;
   constexpr int DY_BYTES = TH * TW * CO * 2;
   constexpr int X_BYTES = (((TH + 2) * (TW + 2) * 128 + 1023) / 1024) * 1024;
   const size_t lds = 2 * (size_t)(DY_BYTES + X_BYTES);
-  auto kfn = wgrad_halo_kernel<CO, TH>;
+  auto kfn = wgrad_halo_kernel<DT, CO, TH>;
   static bool attr = false;
   if (!attr) {
     CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -945,14 +945,14 @@ static int launch_halo(HaloArgs& a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-template <int WC, int WK, int WM, bool FIRST>
+template <int DT, int WC, int WK, int WM, bool FIRST>
 static int launch_wgrad(const WgradArgs& a, hipStream_t s) {
   constexpr int TCo = 64 * WC, TK = 64 * WK;
   constexpr int KSUB = (WM == 1) ? 2 : 1;
   constexpr int BKM = 32 * KSUB * WM;
   size_t lds = 2 * BKM * (TCo + TK) * 2;
   if (WM != 1) lds = std::max(lds, (size_t)(4 * 16 * 64 * 4 + 4 * 4 * 64 * 4) * 4);
-  auto kfn = conv_wgrad_kernel<WC, WK, WM, FIRST>;
+  auto kfn = conv_wgrad_kernel<DT, WC, WK, WM, FIRST>;
   static bool attr = false;
   if (!attr) {
     CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -982,8 +982,10 @@ template <int SG>
 __global__ void __launch_bounds__(256) wgrad_reduce2_kernel(const float* __restrict__ ws, const float* __restrict__ wsb,
                                                             float* __restrict__ dw, float* __restrict__ db, int S,
                                                             int Sb, int Ktot, int Cout, int Cin, int taps, int first,
-                                                            float beta, float scale) {
+                                                            float beta, float scale,
+                                                            const float* __restrict__ dscale) {
   constexpr int EPB = 256 / SG;
+  if (dscale != nullptr) scale *= dscale[0];          // device-side factor (1 / loss scale)
   __shared__ float part[SG][EPB];
   __shared__ float bpart[16][16];
   const int e = threadIdx.x % EPB, grp = threadIdx.x / EPB;
@@ -1054,19 +1056,19 @@ __global__ void __launch_bounds__(256) wgrad_reduce2_kernel(const float* __restr
 }
 
 static int launch_reduce2(const float* ws, const float* wsb, float* dw, float* db, int S, int Sb, int K, int Cout,
-                          int Cin, int taps, int first, float beta, float scale, hipStream_t s) {
+                          int Cin, int taps, int first, float beta, float scale, const float* dscale, hipStream_t s) {
   const size_t plane = (size_t)K * Cout;
   const int nbias = (db != nullptr) ? (Cout + 15) / 16 : 0;
   auto grid = [&](int epb) { return (int)std::min<size_t>((plane + epb - 1) / epb, 4096) + nbias; };
   if (S <= 16)
     hipLaunchKernelGGL(wgrad_reduce2_kernel<1>, dim3(grid(256)), dim3(256), 0, s, ws, wsb, dw, db, S, Sb, K, Cout,
-                       Cin, taps, first, beta, scale);
+                       Cin, taps, first, beta, scale, dscale);
   else if (S <= 128)
     hipLaunchKernelGGL(wgrad_reduce2_kernel<4>, dim3(grid(64)), dim3(256), 0, s, ws, wsb, dw, db, S, Sb, K, Cout,
-                       Cin, taps, first, beta, scale);
+                       Cin, taps, first, beta, scale, dscale);
   else
     hipLaunchKernelGGL(wgrad_reduce2_kernel<16>, dim3(grid(16)), dim3(256), 0, s, ws, wsb, dw, db, S, Sb, K, Cout,
-                       Cin, taps, first, beta, scale);
+                       Cin, taps, first, beta, scale, dscale);
   return (int)hipGetLastError();
 }
 }  // namespace can
@@ -1155,9 +1157,10 @@ static const can::bf16_t* zero_page() {
   return (const can::bf16_t*)z;
 }
 
-extern "C" int can_conv_wgrad(const void* dy, const void* x, float* ws, float* wsb, float* dw, float* db, int N,
-                              int H, int W, int Cin, int Cout, int ksize, int dil, int first, int S, int mslice,
-                              int cfg, float beta, float scale, void* stream) {
+template <int DT>
+static int conv_wgrad_impl(const void* dy, const void* x, float* ws, float* wsb, float* dw, float* db, int N, int H,
+                           int W, int Cin, int Cout, int ksize, int dil, int first, int S, int mslice, int cfg,
+                           float beta, float scale, const float* dscale, void* stream) {
   using namespace can;
   hipStream_t s = (hipStream_t)stream;
   const int K = first ? 64 : ksize * ksize * Cin;
@@ -1171,7 +1174,7 @@ extern "C" int can_conv_wgrad(const void* dy, const void* x, float* ws, float* w
     a.dy = (const bf16_t*)dy; a.x = (const bf16_t*)x; a.ws = ws; a.wsb = wsb_used;
     a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.ksize = ksize; a.dil = dil; a.M = N * H * W;
     a.Ktot = 64; a.S = S; a.mslice = mslice;
-    rc = launch_wgrad<1, 1, 4, true>(a, s);
+    rc = launch_wgrad<DT, 1, 1, 4, true>(a, s);
   } else {
     if (Cin % 64 || Cout % 64 || H < 2 || W < 2) return -3;
     WgradArgs2 a;
@@ -1187,32 +1190,32 @@ extern "C" int can_conv_wgrad(const void* dy, const void* x, float* ws, float* w
       h.N = N; h.H = H; h.W = W; h.Cin = Cin; h.Cout = Cout; h.K = K; h.S = S;
       h.tiles_y = (H + 1) / 2; h.tiles_x = (W + 63) / 64; h.ntiles = N * h.tiles_y * h.tiles_x;
       h.tiles_per_slice = (h.ntiles + S - 1) / S;
-      rc = launch_halo<64, 2>(h, s);   // Cout = 128 runs as two 64-channel co tiles
+      rc = launch_halo<DT, 64, 2>(h, s);   // Cout = 128 runs as two 64-channel co tiles
       if (rc) return rc;
       const int plane = K * Cout;
-      return launch_reduce2(ws, wsb_used, dw, db, S, S, K, Cout, Cin, 9, 0, beta, scale, s);
+      return launch_reduce2(ws, wsb_used, dw, db, S, S, K, Cout, Cin, 9, 0, beta, scale, dscale, s);
     }
     switch (cfg) {
-      case 1: if (Cout % 128) return -4; rc = launch_wgrad2<2, 2, 1, 4, 1, 2>(a, s); break;
-      case 2: if (Cout % 256) return -4; rc = launch_wgrad2<4, 2, 1, 3, 1, 2>(a, s); break;
-      case 3: rc = launch_wgrad2<1, 2, 2, 3, 1, 2>(a, s); break;
-      case 4: rc = launch_wgrad2<1, 1, 2, 4, 1, 2>(a, s); break;
-      case 5: if (Cout % 256) return -4; rc = launch_wgrad2<4, 2, 1, 4, 2, 1>(a, s); break;
-      case 6: if (Cout % 128) return -4; rc = launch_wgrad2<2, 2, 1, 3, 2, 2>(a, s); break;
-      case 7: if (Cout % 256) return -4; rc = launch_wgrad2<4, 2, 1, 2, 2, 2>(a, s); break;
+      case 1: if (Cout % 128) return -4; rc = launch_wgrad2<DT, 2, 2, 1, 4, 1, 2>(a, s); break;
+      case 2: if (Cout % 256) return -4; rc = launch_wgrad2<DT, 4, 2, 1, 3, 1, 2>(a, s); break;
+      case 3: rc = launch_wgrad2<DT, 1, 2, 2, 3, 1, 2>(a, s); break;
+      case 4: rc = launch_wgrad2<DT, 1, 1, 2, 4, 1, 2>(a, s); break;
+      case 5: if (Cout % 256) return -4; rc = launch_wgrad2<DT, 4, 2, 1, 4, 2, 1>(a, s); break;
+      case 6: if (Cout % 128) return -4; rc = launch_wgrad2<DT, 2, 2, 1, 3, 2, 2>(a, s); break;
+      case 7: if (Cout % 256) return -4; rc = launch_wgrad2<DT, 4, 2, 1, 2, 2, 2>(a, s); break;
       case 9:
         if (Cout % 256) return -4;
         if (W % 64 == 0 && Cin % 256 == 0 && mslice % 64 == 0 && (long long)a.M * Cout * 2 < 0x7fffffffLL &&
             Cout <= 2048) {
           if (wsb_used) {
             Sb = kBiasParts;
-            hipLaunchKernelGGL(bias_colsum_kernel, dim3(Sb), dim3(256), 0, s, a.dy, wsb_used, a.M, Cout, Sb);
+            hipLaunchKernelGGL(bias_colsum_kernel<DT>, dim3(Sb), dim3(256), 0, s, a.dy, wsb_used, a.M, Cout, Sb);
           }
           WgradArgs2 g = a;
           g.wsb = nullptr;
-          rc = launch_wgrad3<4, 2, 2>(g, s);
+          rc = launch_wgrad3<DT, 4, 2, 2>(g, s);
         } else
-          rc = launch_wgrad2<4, 2, 1, 2, 2, 2>(a, s);   // same tiles / slicing as cfg 7
+          rc = launch_wgrad2<DT, 4, 2, 1, 2, 2, 2>(a, s);   // same tiles / slicing as cfg 7
         break;
       default: return -5;
     }
@@ -1220,5 +1223,50 @@ extern "C" int can_conv_wgrad(const void* dy, const void* x, float* ws, float* w
   if (rc) return rc;
   const int plane = K * Cout;
   (void)plane;
-  return launch_reduce2(ws, wsb_used, dw, db, S, Sb, K, Cout, first ? 4 : Cin, ksize * ksize, first, beta, scale, s);
+  return launch_reduce2(ws, wsb_used, dw, db, S, Sb, K, Cout, first ? 4 : Cin, ksize * ksize, first, beta, scale, dscale,
+                        s);
+}
+
+// dt: element type of dy / x (DT_BF16 = 0, DT_F16 = 1); the gradients are fp32.  The result is
+// multiplied by scale and, when dscale is not null, by the device scalar dscale[0] (1 / loss scale).
+extern "C" int can_conv_wgrad(const void* dy, const void* x, float* ws, float* wsb, float* dw, float* db, int N,
+                              int H, int W, int Cin, int Cout, int ksize, int dil, int first, int S, int mslice,
+                              int cfg, float beta, float scale, const float* dscale, int dt, void* stream) {
+  CAN_DT_DISPATCH(dt, conv_wgrad_impl<DT>(dy, x, ws, wsb, dw, db, N, H, W, Cin, Cout, ksize, dil, first, S, mslice,
+                                          cfg, beta, scale, dscale, stream));
+}
+
+// Batched 1x1 weight gradient without bias: nb problems dW_b[Cout][Cin] = sum_m dY_b[m][co] X_b[m][ci]
+// (the four conv{S}_2 layers of the context module, one launch instead of four half-filled ones).
+// dY_b = dy + b*dy_bs, X_b = x + b*x_bs (elements), dW_b = dw + b*dw_bs (floats); ws holds nb*S slabs.
+template <int DT>
+static int conv_wgrad_1x1_batched_impl(const void* dy, const void* x, float* ws, float* dw, int M, int W, int Cin,
+                                       int Cout, int nb, long long dy_bs, long long x_bs, long long dw_bs, int S,
+                                       int mslice, float beta, float scale, const float* dscale, hipStream_t s) {
+  using namespace can;
+  if (Cout % 256 || Cin % 256 || W % 64 || mslice % 64 || M % 64 || (long long)M * Cout * 2 >= 0x7fffffffLL) return -3;
+  WgradArgs2 a;
+  a.dy = (const bf16_t*)dy; a.x = (const bf16_t*)x; a.zero = zero_page(); a.ws = ws; a.wsb = nullptr;
+  if (!a.zero) return -7;
+  a.H = M / W; a.W = W; a.Cin = Cin; a.Cout = Cout; a.ksize = 1; a.dil = 1; a.M = M; a.K = Cin;
+  a.S = S; a.mslice = mslice;
+  a.fdW = make_fastdiv((uint32_t)W); a.fdH = make_fastdiv((uint32_t)(M / W)); a.fdC = make_fastdiv((uint32_t)Cin);
+  a.nb = nb; a.dy_bs = dy_bs; a.x_bs = x_bs;
+  int rc = launch_wgrad3<DT, 4, 2, 2>(a, s);
+  if (rc) return rc;
+  const size_t slabs = (size_t)S * Cin * Cout;
+  for (int b = 0; b < nb; ++b) {
+    rc = launch_reduce2(ws + b * slabs, nullptr, dw + b * dw_bs, nullptr, S, S, Cin, Cout, Cin, 1, 0, beta, scale,
+                        dscale, s);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+extern "C" int can_conv_wgrad_1x1_batched(const void* dy, const void* x, float* ws, float* dw, int M, int W, int Cin,
+                                          int Cout, int nb, long long dy_bs, long long x_bs, long long dw_bs, int S,
+                                          int mslice, float beta, float scale, const float* dscale, int dt,
+                                          void* stream) {
+  CAN_DT_DISPATCH(dt, conv_wgrad_1x1_batched_impl<DT>(dy, x, ws, dw, M, W, Cin, Cout, nb, dy_bs, x_bs, dw_bs, S,
+                                                      mslice, beta, scale, dscale, (hipStream_t)stream));
 }

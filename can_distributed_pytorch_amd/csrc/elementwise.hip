@@ -17,21 +17,8 @@
 
 namespace can {
 
-__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
-  const unsigned w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    f[2 * i] = __uint_as_float(w[i] << 16);
-    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
-  }
-}
-__device__ __forceinline__ uint4 pack8(const float* f) {
-  return make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
-}
-// bf16 compare helpers on raw bits (order-preserving map)
-__device__ __forceinline__ float bfv(unsigned short b) { return __uint_as_float(((unsigned)b) << 16); }
-
 // ---------------------------------------------------------------- maxpool
+template <int DT>
 __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const uint4* __restrict__ x, uint4* __restrict__ y, int N,
                                                           int H, int W, int C8) {
   const int Ho = H >> 1, Wo = W >> 1;
@@ -43,19 +30,20 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const uint4* __restric
     const int oy = p % Ho; const int n = p / Ho;
     const size_t base = (((size_t)n * H + 2 * oy) * W + 2 * ox) * C8 + c;
     float a[8], b[8], m[8];
-    unpack8(x[base], m);
-    unpack8(x[base + C8], a);
+    unpack8h<DT>(x[base], m);
+    unpack8h<DT>(x[base + C8], a);
 #pragma unroll
     for (int k = 0; k < 8; ++k) m[k] = fmaxf(m[k], a[k]);
-    unpack8(x[base + (size_t)W * C8], a);
-    unpack8(x[base + (size_t)W * C8 + C8], b);
+    unpack8h<DT>(x[base + (size_t)W * C8], a);
+    unpack8h<DT>(x[base + (size_t)W * C8 + C8], b);
 #pragma unroll
     for (int k = 0; k < 8; ++k) m[k] = fmaxf(m[k], fmaxf(a[k], b[k]));
-    y[i] = pack8(m);  // exact: max of bf16 values is a bf16 value
+    y[i] = pack8h<DT>(m);  // exact: max of bf16 values is a bf16 value
   }
 }
 
 // dx[full] = (x is the first max of its window) * (x > 0) * dy[pooled]
+template <int DT>
 __global__ void __launch_bounds__(256) maxpool_bwd_relu_kernel(const uint4* __restrict__ x, const uint4* __restrict__ dy,
                                                                uint4* __restrict__ dx, int N, int H, int W, int C8) {
   const int Ho = H >> 1, Wo = W >> 1;
@@ -69,8 +57,8 @@ __global__ void __launch_bounds__(256) maxpool_bwd_relu_kernel(const uint4* __re
     const size_t off[4] = {b0, b0 + C8, b0 + (size_t)W * C8, b0 + (size_t)W * C8 + C8};
     float v[4][8], g[8];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) unpack8(x[off[q]], v[q]);
-    unpack8(dy[i], g);
+    for (int q = 0; q < 4; ++q) unpack8h<DT>(x[off[q]], v[q]);
+    unpack8h<DT>(dy[i], g);
     float o[4][8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -85,12 +73,13 @@ __global__ void __launch_bounds__(256) maxpool_bwd_relu_kernel(const uint4* __re
       for (int q = 0; q < 4; ++q) o[q][k] = (q == arg) ? gg : 0.f;
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) dx[off[q]] = pack8(o[q]);
+    for (int q = 0; q < 4; ++q) dx[off[q]] = pack8h<DT>(o[q]);
   }
 }
 
 // ---------------------------------------------------------------- head
 // et[p] = sum_c y[p][c] * w[c] + b      (y: [P][64] bf16 post-ReLU)
+template <int DT>
 __global__ void __launch_bounds__(256) head_fwd_kernel(const uint4* __restrict__ y, const float* __restrict__ w,
                                                        const float* __restrict__ b, float* __restrict__ et, int P) {
   // 8 lanes per pixel (8 channels each)
@@ -101,7 +90,7 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(const uint4* __restrict__
   const float bias = b[0];
   for (size_t p = ((size_t)blockIdx.x * 256 + threadIdx.x) >> 3; p < (size_t)P; p += ((size_t)gridDim.x * 256) >> 3) {
     float v[8];
-    unpack8(y[p * 8 + lane8], v);
+    unpack8h<DT>(y[p * 8 + lane8], v);
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) s += v[k] * wl[k];
@@ -113,13 +102,16 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(const uint4* __restrict__
 }
 
 // Training head: et = y.w + b; loss = sum (et-gt)^2; det = 2(et-gt)*gscale;
-// dy[p][c] = det * w[c] * (y > 0); partial dw[c] = sum_p det*y[p][c], db = sum det.
+// dy[p][c] = det * S * w[c] * (y > 0) (S = device loss scale, 1 if null); partial dw[c] = sum_p det*y[p][c], db = sum det.
 // Per-block partials -> part[block][66] (64 dw, db, loss); reduced by head_reduce.
+template <int DT>
 __global__ void __launch_bounds__(256) head_train_kernel(const uint4* __restrict__ y, const float* __restrict__ w,
                                                          const float* __restrict__ b, const float* __restrict__ gt,
                                                          float* __restrict__ et, uint4* __restrict__ dy,
-                                                         float* __restrict__ part, int P, float gscale) {
+                                                         float* __restrict__ part, int P, float gscale,
+                                                         const float* __restrict__ lscale) {
   __shared__ float red[256 / 8][66];
+  const float dys = (lscale != nullptr) ? lscale[0] : 1.f;   // loss scale: applied to dy only
   const int lane8 = threadIdx.x & 7;
   const int pg = threadIdx.x >> 3;
   float wl[8], dwl[8];
@@ -129,7 +121,7 @@ __global__ void __launch_bounds__(256) head_train_kernel(const uint4* __restrict
   float dbl = 0.f, lossl = 0.f;
   for (size_t p = ((size_t)blockIdx.x * 256 + threadIdx.x) >> 3; p < (size_t)P; p += ((size_t)gridDim.x * 256) >> 3) {
     float v[8];
-    unpack8(y[p * 8 + lane8], v);
+    unpack8h<DT>(y[p * 8 + lane8], v);
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) s += v[k] * wl[k];
@@ -143,10 +135,10 @@ __global__ void __launch_bounds__(256) head_train_kernel(const uint4* __restrict
     float o[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      o[k] = (v[k] > 0.f) ? g * wl[k] : 0.f;
+      o[k] = (v[k] > 0.f) ? g * dys * wl[k] : 0.f;
       dwl[k] += g * v[k];
     }
-    dy[p * 8 + lane8] = pack8(o);
+    dy[p * 8 + lane8] = pack8h<DT>(o);
   }
 #pragma unroll
   for (int k = 0; k < 8; ++k) red[pg][lane8 * 8 + k] = dwl[k];
@@ -193,13 +185,14 @@ __global__ void __launch_bounds__(1024) head_reduce_kernel(const float* __restri
 // ---------------------------------------------------------------- SGD
 // torch.optim.SGD semantics (dampening 0, nesterov False, wd 0):
 //   buf = g (first step) | momentum*buf + g ;  p -= lr*buf,  g = grad*gscale.
-// flags[0] != 0 (non-finite loss) -> the whole update is skipped (graph-safe,
+// flags[0] != 0 (non-finite loss) or flags[2] != 0 (non-finite gradient, set by
+// grad_nonfinite in the fp16 step) -> the whole update is skipped (graph-safe,
 // no host sync).  Vectorised float4 over a 16-B aligned arena.
 __global__ void __launch_bounds__(256) sgd_momentum_kernel(float4* __restrict__ p, float4* __restrict__ buf,
                                                            const float4* __restrict__ g, size_t n4, float lr,
                                                            float momentum, float gscale, int first,
                                                            const float* __restrict__ flags) {
-  if (flags != nullptr && flags[0] != 0.f) return;
+  if (flags != nullptr && (flags[0] != 0.f || flags[2] != 0.f)) return;
   for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
     float4 gv = g[i];
     gv.x *= gscale; gv.y *= gscale; gv.z *= gscale; gv.w *= gscale;
@@ -217,9 +210,44 @@ __global__ void __launch_bounds__(256) sgd_momentum_kernel(float4* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------- loss scaling
+// Dynamic loss scaling for the fp16 step, entirely device-side (graph-safe):
+// grad_nonfinite ORs "some gradient is inf/NaN" into *flag (the step's
+// flags[2], which the fused SGD skips on); scale_update then backs the scale
+// off on overflow or grows it after `interval` clean steps.
+// scaler = {S, 1/S, clean steps, 0}.
+__global__ void __launch_bounds__(256) grad_nonfinite_kernel(const float4* __restrict__ g, size_t n4,
+                                                             float* __restrict__ flag) {
+  bool bad = false;
+  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+    const float4 v = g[i];
+    bad |= !(isfinite(v.x) && isfinite(v.y) && isfinite(v.z) && isfinite(v.w));
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<int*>(flag), 0x3f800000);   // 1.0f
+}
+
+__global__ void scale_update_kernel(const float* __restrict__ flag, float* __restrict__ scaler, int interval,
+                                    float growth, float backoff, float max_scale) {
+  if (threadIdx.x != 0) return;
+  float S = scaler[0], n = scaler[2];
+  if (flag[0] != 0.f) {
+    S = fmaxf(S * backoff, 1.f);
+    n = 0.f;
+  } else if (n + 1.f >= (float)interval) {
+    S = fminf(S * growth, max_scale);
+    n = 0.f;
+  } else {
+    n += 1.f;
+  }
+  scaler[0] = S;
+  scaler[1] = 1.f / S;
+  scaler[2] = n;
+}
+
 // ---------------------------------------------------------------- packing
 // w fp32 [Co][Ci][k][k] -> fwd bf16 [Co][tap][Ci] and dgrad bf16 [Ci][8-tap][Co]
 // (first layer: fwd [Co][64] with k = tap*4 + c, no dgrad).
+template <int DT>
 __global__ void __launch_bounds__(256) pack_conv_kernel(const float* __restrict__ w, bf16_t* __restrict__ fwd,
                                                         bf16_t* __restrict__ dgr, int Co, int Ci, int taps,
                                                         int first) {
@@ -229,7 +257,7 @@ __global__ void __launch_bounds__(256) pack_conv_kernel(const float* __restrict_
     const size_t r = i / taps;
     const int ci = r % Ci;
     const int co = r / Ci;
-    const unsigned short v = f2bf(w[i]);
+    const unsigned short v = f2h<DT>(w[i]);
     if (first) {
       fwd[(size_t)co * 64 + tap * 4 + ci] = v;
     } else {
@@ -244,6 +272,7 @@ __global__ void __launch_bounds__(256) pack_conv_kernel(const float* __restrict_
 // 32(ci) x taps tile transposed through LDS, so the fp32 reads (ci, tap
 // contiguous per co), the fwd-pack writes (ci contiguous per co, tap) and the
 // dgrad-pack writes (co contiguous per ci, tap) are all coalesced.
+template <int DT>
 __global__ void __launch_bounds__(256) pack_multi_kernel(const long long* __restrict__ desc) {
   __shared__ unsigned short t[32][32 * 9 + 2];       // [co][ci*taps + tap] bf16 bits
   const long long* d = desc + (size_t)blockIdx.y * 8;
@@ -258,7 +287,7 @@ __global__ void __launch_bounds__(256) pack_multi_kernel(const long long* __rest
   const int row = cis * taps;                          // contiguous floats per co in the tile
   for (int i = threadIdx.x; i < cos_ * row; i += 256) {
     const int c = i / row, r = i - c * row;
-    t[c][r] = f2bf(w[((size_t)(co0 + c) * Ci + ci0) * taps + r]);
+    t[c][r] = f2h<DT>(w[((size_t)(co0 + c) * Ci + ci0) * taps + r]);
   }
   __syncthreads();
   if (first) {
@@ -283,6 +312,7 @@ __global__ void __launch_bounds__(256) pack_multi_kernel(const long long* __rest
 }
 
 // [N,3,H,W] fp32 -> [N,H,W,4] bf16 (4th channel zero)
+template <int DT>
 __global__ void __launch_bounds__(256) img_to_nhwc4_kernel(const float* __restrict__ img, uint2* __restrict__ out,
                                                            int N, int H, int W) {
   const size_t HW = (size_t)H * W;
@@ -290,7 +320,7 @@ __global__ void __launch_bounds__(256) img_to_nhwc4_kernel(const float* __restri
   for (size_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
     const size_t n = i / HW, p = i % HW;
     const float* b = img + n * 3 * HW + p;
-    out[i] = make_uint2(pack2bf(b[0], b[HW]), pack2bf(b[2 * HW], 0.f));
+    out[i] = make_uint2(pack2<DT>(b[0], b[HW]), pack2<DT>(b[2 * HW], 0.f));
   }
 }
 
@@ -305,35 +335,42 @@ static inline int grid_for(size_t n, int per = 256, int cap = 4096) {
 
 using namespace can;
 
-extern "C" int can_maxpool_fwd(const void* x, void* y, int N, int H, int W, int C, void* stream) {
+extern "C" int can_maxpool_fwd(const void* x, void* y, int N, int H, int W, int C, int dt, void* stream) {
   if ((C & 7) || (H & 1) || (W & 1)) return -2;
   const size_t tot = (size_t)N * (H / 2) * (W / 2) * (C / 8);
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(tot, 256, 8192)), dim3(256), 0, (hipStream_t)stream,
-                     (const uint4*)x, (uint4*)y, N, H, W, C / 8);
+  CAN_LAUNCH_DT(dt, maxpool_fwd_kernel, dim3(grid_for(tot, 256, 8192)), dim3(256), 0,
+                (hipStream_t)stream, (const uint4*)x, (uint4*)y, N, H, W, C / 8);
   return (int)hipGetLastError();
 }
 
-extern "C" int can_maxpool_bwd_relu(const void* x, const void* dy, void* dx, int N, int H, int W, int C,
+extern "C" int can_maxpool_bwd_relu(const void* x, const void* dy, void* dx, int N, int H, int W, int C, int dt,
                                     void* stream) {
   if ((C & 7) || (H & 1) || (W & 1)) return -2;
   const size_t tot = (size_t)N * (H / 2) * (W / 2) * (C / 8);
-  hipLaunchKernelGGL(maxpool_bwd_relu_kernel, dim3(grid_for(tot, 256, 8192)), dim3(256), 0, (hipStream_t)stream,
-                     (const uint4*)x, (const uint4*)dy, (uint4*)dx, N, H, W, C / 8);
+  CAN_LAUNCH_DT(dt, maxpool_bwd_relu_kernel, dim3(grid_for(tot, 256, 8192)), dim3(256), 0,
+                (hipStream_t)stream, (const uint4*)x, (const uint4*)dy, (uint4*)dx, N, H, W,
+                C / 8);
   return (int)hipGetLastError();
 }
 
-extern "C" int can_head_fwd(const void* y, const float* w, const float* b, float* et, int P, void* stream) {
-  hipLaunchKernelGGL(head_fwd_kernel, dim3(grid_for((size_t)P * 8, 256, 2048)), dim3(256), 0, (hipStream_t)stream,
-                     (const uint4*)y, w, b, et, P);
+extern "C" int can_head_fwd(const void* y, const float* w, const float* b, float* et, int P, int dt, void* stream) {
+  CAN_LAUNCH_DT(dt, head_fwd_kernel, dim3(grid_for((size_t)P * 8, 256, 2048)), dim3(256),
+                0, (hipStream_t)stream, (const uint4*)y, w, b, et, P);
   return (int)hipGetLastError();
 }
 
 extern "C" int can_head_train(const void* y, const float* w, const float* b, const float* gt, float* et, void* dy,
                               float* part, int nblk, float* dw, float* db, float* loss, int P, float gscale,
-                              float beta, void* stream) {
+                              float beta, const float* lscale, int dt, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(head_train_kernel, dim3(nblk), dim3(256), 0, s, (const uint4*)y, w, b, gt, et, (uint4*)dy, part,
-                     P, gscale);
+  if (dt == DT_F16)
+    hipLaunchKernelGGL(head_train_kernel<DT_F16>, dim3(nblk), dim3(256), 0, s, (const uint4*)y, w, b, gt, et,
+                       (uint4*)dy, part, P, gscale, lscale);
+  else if (dt == DT_BF16)
+    hipLaunchKernelGGL(head_train_kernel<DT_BF16>, dim3(nblk), dim3(256), 0, s, (const uint4*)y, w, b, gt, et,
+                       (uint4*)dy, part, P, gscale, lscale);
+  else
+    return -20;
   hipLaunchKernelGGL(head_reduce_kernel, dim3(1), dim3(1024), 0, s, part, nblk, dw, db, loss, beta);
   return (int)hipGetLastError();
 }
@@ -346,22 +383,38 @@ extern "C" int can_sgd_momentum(float* p, float* buf, const float* g, size_t n, 
   return (int)hipGetLastError();
 }
 
-extern "C" int can_pack_conv(const float* w, void* fwd, void* dgr, int Co, int Ci, int taps, int first,
+extern "C" int can_grad_nonfinite(const float* g, size_t n, float* flag, void* stream) {
+  if (n & 3) return -2;
+  hipLaunchKernelGGL(grad_nonfinite_kernel, dim3(grid_for(n / 4, 256, 2048)), dim3(256), 0, (hipStream_t)stream,
+                     (const float4*)g, n / 4, flag);
+  return (int)hipGetLastError();
+}
+
+extern "C" int can_scale_update(const float* flag, float* scaler, int interval, float growth, float backoff,
+                                float max_scale, void* stream) {
+  hipLaunchKernelGGL(scale_update_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, flag, scaler, interval, growth,
+                     backoff, max_scale);
+  return (int)hipGetLastError();
+}
+
+extern "C" int can_pack_conv(const float* w, void* fwd, void* dgr, int Co, int Ci, int taps, int first, int dt,
                              void* stream) {
-  hipLaunchKernelGGL(pack_conv_kernel, dim3(grid_for((size_t)Co * Ci * taps, 256, 4096)), dim3(256), 0,
-                     (hipStream_t)stream, w, (bf16_t*)fwd, (bf16_t*)dgr, Co, Ci, taps, first);
+  CAN_LAUNCH_DT(dt, pack_conv_kernel, dim3(grid_for((size_t)Co * Ci * taps, 256, 4096)),
+                dim3(256), 0, (hipStream_t)stream, w, (bf16_t*)fwd, (bf16_t*)dgr, Co, Ci,
+                taps, first);
   return (int)hipGetLastError();
 }
 
-extern "C" int can_img_to_nhwc4(const float* img, void* out, int N, int H, int W, void* stream) {
-  hipLaunchKernelGGL(img_to_nhwc4_kernel, dim3(grid_for((size_t)N * H * W, 256, 8192)), dim3(256), 0,
-                     (hipStream_t)stream, img, (uint2*)out, N, H, W);
+extern "C" int can_img_to_nhwc4(const float* img, void* out, int N, int H, int W, int dt, void* stream) {
+  CAN_LAUNCH_DT(dt, img_to_nhwc4_kernel, dim3(grid_for((size_t)N * H * W, 256, 8192)),
+                dim3(256), 0, (hipStream_t)stream, img, (uint2*)out, N, H, W);
   return (int)hipGetLastError();
 }
 
-extern "C" int can_pack_multi(const long long* desc, int layers, int max_tiles, void* stream) {
+extern "C" int can_pack_multi(const long long* desc, int layers, int max_tiles, int dt, void* stream) {
   if (layers <= 0) return 0;
   // grid.x covers the largest layer's 32x32 tiles (B1: 512 -> 1024 channels = 512 tiles)
-  hipLaunchKernelGGL(pack_multi_kernel, dim3(max_tiles, layers), dim3(256), 0, (hipStream_t)stream, desc);
+  CAN_LAUNCH_DT(dt, pack_multi_kernel, dim3(max_tiles, layers), dim3(256), 0,
+                (hipStream_t)stream, desc);
   return (int)hipGetLastError();
 }

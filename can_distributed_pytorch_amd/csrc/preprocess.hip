@@ -23,6 +23,7 @@ __device__ __forceinline__ void lin_tap(int o, float scale, int in, int& i0, int
 }
 
 // img: uint8 [H0][W0][C] (C = 1, 3 or 4) -> out NHWC4 bf16 [Ho][Wo][4] (sample n of a batch)
+template <int DT>
 __global__ void __launch_bounds__(256) preprocess_image_kernel(const unsigned char* __restrict__ img, int H0, int W0,
                                                                int C, int flip, uint2* __restrict__ out, int Ho,
                                                                int Wo, float m0, float m1, float m2, float is0,
@@ -48,7 +49,7 @@ __global__ void __launch_bounds__(256) preprocess_image_kernel(const unsigned ch
       const float top = a + (b - a) * fx, bot = d + (e - d) * fx;
       v[c] = (top + (bot - top) * fy) * (1.f / 255.f);
     }
-    out[i] = make_uint2(pack2bf((v[0] - m0) * is0, (v[1] - m1) * is1), pack2bf((v[2] - m2) * is2, 0.f));
+    out[i] = make_uint2(pack2<DT>((v[0] - m0) * is0, (v[1] - m1) * is1), pack2<DT>((v[2] - m2) * is2, 0.f));
   }
 }
 
@@ -73,15 +74,15 @@ __global__ void __launch_bounds__(256) preprocess_density_kernel(const float* __
 
 }  // namespace can
 
-extern "C" int can_preprocess_image(const void* img, int H0, int W0, int C, int flip, void* out, int Ho, int Wo,
+extern "C" int can_preprocess_image(const void* img, int H0, int W0, int C, int flip, void* out, int Ho, int Wo, int dt,
                                     void* stream) {
   using namespace can;
   if (C != 1 && C != 3 && C != 4) return -2;
   const int total = Ho * Wo;
   const int grid = (total + 255) / 256 > 4096 ? 4096 : (total + 255) / 256;
-  hipLaunchKernelGGL(preprocess_image_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const unsigned char*)img,
-                     H0, W0, C, flip, (uint2*)out, Ho, Wo, 0.485f, 0.456f, 0.406f, 1.f / 0.229f, 1.f / 0.224f,
-                     1.f / 0.225f);
+  CAN_LAUNCH_DT(dt, preprocess_image_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const unsigned char*)img,
+                H0, W0, C, flip, (uint2*)out, Ho, Wo, 0.485f, 0.456f, 0.406f, 1.f / 0.229f, 1.f / 0.224f,
+                1.f / 0.225f);
   return (int)hipGetLastError();
 }
 

@@ -17,7 +17,14 @@ re-designed for MI355X:
 * the bf16 weight packs are refreshed by pack kernels right after SGD;
 * with ``graph=True`` the whole step (for a fixed input shape) is captured
   once into a hipGraph (torch.cuda.CUDAGraph) and replayed: one launch per
-  step instead of ~150 kernel launches.
+  step instead of ~150 kernel launches;
+* ``dtype="fp16"`` runs the same kernels on fp16 activations / weight packs
+  (v_mfma_f32_16x16x32_f16) with dynamic loss scaling kept on the device
+  (graph-safe): the scale multiplies d(b6) inside the fused head, 1/scale is
+  folded into every weight-gradient reduction, a gradient-overflow check
+  after the all-reduce makes the fused SGD skip the step, and a one-thread
+  kernel backs the scale off / grows it (GradScaler semantics: x0.5 on
+  overflow, x2 after ``scale_interval`` clean steps).
 """
 from __future__ import annotations
 
@@ -31,14 +38,18 @@ from ..ops import _ext
 from ..ops.executor import CANNetExecutor
 from ..utils.flat import FlatArena
 
+ACT_DTYPES = {"bf16": torch.bfloat16, "fp16": torch.float16}
+
 
 class NativeStepper:
     def __init__(self, device, dtype="bf16", world=1, lr=1e-7, momentum=0.95, batch=8, height=768, width=1024,
                  graph=True, model: Optional[CANNet] = None, reducer=None, bucket_mb: float = 25.0,
-                 reducer_transport: Optional[str] = None):
-        if dtype != "bf16":
-            raise ValueError("the native step computes in bf16 (fp32 master weights); use --impl torch for fp32")
+                 reducer_transport: Optional[str] = None, init_scale: float = 65536.0, scale_interval: int = 2000):
+        if dtype not in ACT_DTYPES:
+            raise ValueError(f"the native step computes in bf16 or fp16 (fp32 master weights), got {dtype!r}; "
+                             "use --impl torch for fp32")
         self.C = _ext.require()
+        self.dtype = dtype
         self.device = torch.device(device)
         self.model = (model or CANNet(backend="hip")).to(self.device)
         self.model.exec_backend = "hip"
@@ -46,13 +57,19 @@ class NativeStepper:
         self.lr = lr * world                       # train.py:25 linear scaling
         self.momentum = momentum
         self.params = list(self.model.parameters())
-        self.ex = CANNetExecutor(self.model)
+        self.ex = CANNetExecutor(self.model, dtype=ACT_DTYPES[dtype])
         self.model._executor = self.ex
         # fp32 master/grad arenas laid out in gradient-ready order (contiguous buckets)
         self.arena = FlatArena(self.params, self.device, order=self.ex.grad_ready_order())
         self.mom = torch.zeros_like(self.arena.data)  # momentum buffer (zero init == torch's first-step clone)
         self.grads = self.arena.grad_views()
-        self.flags = torch.zeros(4, dtype=torch.float32, device=self.device)   # [nonfinite, loss, ...]
+        self.flags = torch.zeros(4, dtype=torch.float32, device=self.device)   # [nonfinite loss, loss, grad overflow, 0]
+        # fp16: device-side dynamic loss scale {S, 1/S, clean steps, 0}
+        self.scaler = None
+        self.scale_interval = scale_interval
+        if dtype == "fp16":
+            self.scaler = torch.tensor([init_scale, 1.0 / init_scale, 0.0, 0.0], dtype=torch.float32,
+                                       device=self.device)
         self.reducer = reducer
         if self.reducer is None and (world > 1 or reducer_transport is not None):
             from ..parallel.reducer import BucketedReducer
@@ -81,12 +98,14 @@ class NativeStepper:
         st = _ext.stream_ptr(self.device)
         b6, sv = ex.forward_features(img, save=True)
         ex.workspace(*ex.input_hw(img))
-        loss, et, d_b6 = ex.head_train(b6, gt, self.grads)
+        sc = self.scaler
+        loss, et, d_b6 = ex.head_train(b6, gt, self.grads, lscale=sc[0:1] if sc is not None else None)
         red = self.reducer
         if red is not None:
             red.begin()
             red.mark_ready([ex.head_w_index, ex.head_b_index])
-        ex.backward_features(sv, d_b6, self.grads, on_grad_ready=(red.mark_ready if red is not None else None))
+        ex.backward_features(sv, d_b6, self.grads, on_grad_ready=(red.mark_ready if red is not None else None),
+                             dscale=sc[1:2] if sc is not None else None)
         del sv
         # scalars: [nonfinite flag, loss]
         self.flags[0:1].copy_((~torch.isfinite(loss)).float())
@@ -94,12 +113,19 @@ class NativeStepper:
         if red is not None:
             red.finish()
             red.allreduce_scalars(self.flags[0:2])
+        if sc is not None:
+            # after the all-reduce every rank holds the same gradients -> the same verdict
+            self.flags[2:3].zero_()
+            self.C.grad_nonfinite(self.arena.grad.data_ptr(), self.arena.numel, self.flags.data_ptr() + 8, st)
         if not update:
             return self.flags[1:2]
         gscale = 1.0 / self.world
         self.C.sgd_momentum(self.arena.data.data_ptr(), self.mom.data_ptr(), self.arena.grad.data_ptr(),
                             self.arena.numel, float(self.lr), float(self.momentum), float(gscale), 0,
                             self.flags.data_ptr(), st)
+        if sc is not None:
+            self.C.scale_update(self.flags.data_ptr() + 8, sc.data_ptr(), int(self.scale_interval), 2.0, 0.5,
+                                float(2 ** 24), st)
         ex.refresh_packs(force=True)
         ex.mark_weights_updated()
         return self.flags[1:2]
@@ -141,4 +167,14 @@ class NativeStepper:
         return None if self._loss is None else float(self._loss.reshape(-1)[0])
 
     def nonfinite(self) -> bool:
+        """Non-finite loss in the last step (the reference's exit condition).  An fp16 gradient overflow
+        is not one: that step is skipped and the loss scale backed off."""
         return bool(self.flags[0].item() != 0)
+
+    def loss_scale(self) -> float:
+        return 1.0 if self.scaler is None else float(self.scaler[0].item())
+
+    def skipped_last(self) -> bool:
+        """True when the last step's update was skipped (non-finite loss or gradient)."""
+        f = self.flags.tolist()
+        return f[0] != 0 or f[2] != 0

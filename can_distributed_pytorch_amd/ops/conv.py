@@ -1,14 +1,18 @@
 """Python front-end of the gfx950 implicit-GEMM convolution kernels.
 
 Replaces the nn.Conv2d calls of the reference (model/CANNet.py:14-17,114-115)
-with NHWC bf16 MFMA kernels (csrc/conv_igemm.hip forward + data-gradient,
+with NHWC 16-bit MFMA kernels (csrc/conv_igemm.hip forward + data-gradient,
 csrc/conv_wgrad.hip weight-gradient).  All shape / dtype / layout checks are
 done here, on the host, before anything is launched.
 
+Element type: bf16 (default) or fp16, taken from the activation tensor; every
+16-bit operand of one call must share it (v_mfma_f32_16x16x32_{bf16,f16},
+fp32 accumulation either way).
+
 Weight layouts (packed from the fp32 master weights [Co][Ci][kh][kw]):
-  * forward  : [Co][kh][kw][Ci] bf16   (K = 9*Ci contiguous per output channel)
-  * dgrad    : [Ci][kh'][kw'][Co] bf16 with kh' = 2-kh, kw' = 2-kw (flipped)
-  * first    : [64][64] bf16, k = tap*4 + c (c < 3), zero padded (Cin=3 layer)
+  * forward  : [Co][kh][kw][Ci]        (K = 9*Ci contiguous per output channel)
+  * dgrad    : [Ci][kh'][kw'][Co] with kh' = 2-kh, kw' = 2-kw (flipped)
+  * first    : [64][64], k = tap*4 + c (c < 3), zero padded (Cin=3 layer)
 """
 from __future__ import annotations
 
@@ -20,40 +24,49 @@ from . import _ext
 
 EPI_BIAS_RELU, EPI_MASK, EPI_NONE, EPI_BIAS = 0, 1, 2, 3
 BF16 = torch.bfloat16
+ACT_DTYPES = {torch.bfloat16: 0, torch.float16: 1}   # -> kernel element-type code (csrc/common.h DT_*)
 
 
-def pack_weight_fwd(w: torch.Tensor) -> torch.Tensor:
+def dt_code(dtype: torch.dtype) -> int:
+    if dtype not in ACT_DTYPES:
+        raise ValueError(f"native kernels take bf16 or fp16 activations, got {dtype}")
+    return ACT_DTYPES[dtype]
+
+
+def pack_weight_fwd(w: torch.Tensor, dtype: torch.dtype = BF16) -> torch.Tensor:
     co = w.shape[0]
-    return w.detach().permute(0, 2, 3, 1).reshape(co, -1).to(BF16).contiguous()
+    return w.detach().permute(0, 2, 3, 1).reshape(co, -1).to(dtype).contiguous()
 
 
-def pack_weight_dgrad(w: torch.Tensor) -> torch.Tensor:
+def pack_weight_dgrad(w: torch.Tensor, dtype: torch.dtype = BF16) -> torch.Tensor:
     ci = w.shape[1]
-    return w.detach().flip(2, 3).permute(1, 2, 3, 0).reshape(ci, -1).to(BF16).contiguous()
+    return w.detach().flip(2, 3).permute(1, 2, 3, 0).reshape(ci, -1).to(dtype).contiguous()
 
 
-def pack_weight_first(w: torch.Tensor) -> torch.Tensor:
+def pack_weight_first(w: torch.Tensor, dtype: torch.dtype = BF16) -> torch.Tensor:
     co, ci, kh, kw = w.shape
     assert ci == 3 and kh == 3 and kw == 3
     wp = torch.zeros(co, 64, dtype=torch.float32, device=w.device)
     wp[:, :36].view(co, 9, 4)[:, :, :3] = w.detach().float().permute(0, 2, 3, 1).reshape(co, 9, 3)
-    return wp.to(BF16).contiguous()
+    return wp.to(dtype).contiguous()
 
 
-def to_nhwc4(img: torch.Tensor) -> torch.Tensor:
-    """[N,3,H,W] float -> [N,H,W,4] bf16 (channel 3 = 0): the first layer's input layout."""
+def to_nhwc4(img: torch.Tensor, dtype: torch.dtype = BF16) -> torch.Tensor:
+    """[N,3,H,W] float -> [N,H,W,4] 16-bit (channel 3 = 0): the first layer's input layout."""
     n, c, h, w = img.shape
     assert c == 3
-    out = torch.zeros(n, h, w, 4, dtype=BF16, device=img.device)
+    out = torch.zeros(n, h, w, 4, dtype=dtype, device=img.device)
     out[..., :3] = img.permute(0, 2, 3, 1)
     return out
 
 
-def _check_act(x: torch.Tensor, name: str, c: Optional[int] = None):
+def _check_act(x: torch.Tensor, name: str, c: Optional[int] = None, dtype: Optional[torch.dtype] = None):
     if not x.is_cuda:
         raise ValueError(f"{name} must be a GPU tensor")
-    if x.dtype != BF16:
-        raise ValueError(f"{name} must be bf16, got {x.dtype}")
+    if x.dtype not in ACT_DTYPES:
+        raise ValueError(f"{name} must be bf16 or fp16, got {x.dtype}")
+    if dtype is not None and x.dtype != dtype:
+        raise ValueError(f"{name} is {x.dtype}, the other operands are {dtype}")
     if not x.is_contiguous():
         raise ValueError(f"{name} must be contiguous NHWC")
     if c is not None and x.shape[-1] != c:
@@ -70,8 +83,9 @@ def conv_igemm(x: torch.Tensor, wpack: torch.Tensor, bias: Optional[torch.Tensor
     n, h, w, ci = x.shape
     _check_act(x, "x")
     co, k = wpack.shape
-    if wpack.dtype != BF16 or not wpack.is_contiguous():
-        raise ValueError("wpack must be contiguous bf16")
+    dt = x.dtype
+    if wpack.dtype != dt or not wpack.is_contiguous():
+        raise ValueError(f"wpack must be contiguous {dt}")
     if first:
         if ci != 4 or ksize != 3 or k != 64:
             raise ValueError("first-layer conv expects x[...,4], 3x3, packed weight [Co,64]")
@@ -90,18 +104,18 @@ def conv_igemm(x: torch.Tensor, wpack: torch.Tensor, bias: Optional[torch.Tensor
     if epi == EPI_MASK:
         if mask is None or tuple(mask.shape) != (n, h, w, co):
             raise ValueError("mask must be [N,H,W,Cout]")
-        _check_act(mask, "mask")
+        _check_act(mask, "mask", dtype=dt)
     if out is None:
-        out = torch.empty(n, h, w, co, dtype=BF16, device=x.device)
+        out = torch.empty(n, h, w, co, dtype=dt, device=x.device)
     else:
         if tuple(out.shape) != (n, h, w, co):
             raise ValueError("out has the wrong shape")
-        _check_act(out, "out")
+        _check_act(out, "out", dtype=dt)
     if n * h * w >= 2 ** 31 // max(ci, co):
         raise ValueError("tensor too large for 32-bit pixel indexing")
     C.conv_igemm(x.data_ptr(), wpack.data_ptr(), bias.data_ptr() if bias is not None else 0,
                  mask.data_ptr() if mask is not None else 0, out.data_ptr(), n, h, w, ci, co, ksize, dil,
-                 epi, int(first), tile, _ext.stream_ptr(x.device))
+                 epi, int(first), tile, dt_code(dt), _ext.stream_ptr(x.device))
     return out
 
 
@@ -129,11 +143,14 @@ class WgradWorkspace:
 
 def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, db: Optional[torch.Tensor], *, ksize: int,
                dil: int = 1, first: bool = False, ws: Optional[WgradWorkspace] = None, beta: float = 0.0,
-               scale: float = 1.0) -> None:
-    """dw[Co,Ci,kh,kw] (fp32, PyTorch layout) = scale * sum_m dY[m,co] Xcol[m,k] (+ beta*dw); db likewise."""
+               scale: float = 1.0, dscale: Optional[torch.Tensor] = None) -> None:
+    """dw[Co,Ci,kh,kw] (fp32, PyTorch layout) = scale * [dscale[0]] * sum_m dY[m,co] Xcol[m,k] (+ beta*dw);
+    db likewise.  dscale: optional fp32 device scalar read at run time (1 / loss scale of the fp16 step)."""
     C = _ext.require()
     _check_act(dy, "dy")
-    _check_act(x, "x")
+    _check_act(x, "x", dtype=dy.dtype)
+    if dscale is not None and (dscale.dtype != torch.float32 or not dscale.is_cuda):
+        raise ValueError("dscale must be an fp32 GPU tensor")
     n, h, w, ci = x.shape
     co = dy.shape[-1]
     if tuple(dy.shape[:3]) != (n, h, w):
@@ -157,4 +174,51 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, db: Optional
     wsb_ptr = buf.data_ptr() + 4 * s * ktot * co
     C.conv_wgrad(dy.data_ptr(), x.data_ptr(), buf.data_ptr(), wsb_ptr, dw.data_ptr(),
                  db.data_ptr() if db is not None else 0, n, h, w, ci, co, ksize, dil, int(first), s, mslice, cfg,
-                 float(beta), float(scale), _ext.stream_ptr(x.device))
+                 float(beta), float(scale), dscale.data_ptr() if dscale is not None else 0, dt_code(dy.dtype),
+                 _ext.stream_ptr(x.device))
+
+
+def wgrad_1x1_batched_plan(m: int, nb: int, ci: int, co: int, ncu: int = 256):
+    """(S, mslice, workspace floats) of the batched 1x1 weight gradient: one round of 256x256 tiles over the CUs."""
+    ntile = (co // 256) * (ci // 256) * nb
+    s = max(1, ncu // ntile)
+    mslice = -(-m // s)
+    mslice = -(-mslice // 64) * 64
+    s = -(-m // mslice)
+    return s, mslice, nb * s * ci * co
+
+
+def wgrad_1x1_batched_ok(dy: torch.Tensor, x: torch.Tensor, dws) -> bool:
+    """Shapes / layouts the batched kernel takes: [nb,N,H,W,C] operands with W % 64 == 0, channels % 256 == 0,
+    and the nb fp32 [Co,Ci,1,1] outputs laid out back to back (consecutive slots of the gradient arena)."""
+    if dy.dim() != 5 or x.dim() != 5 or not (dy.is_contiguous() and x.is_contiguous()):
+        return False
+    nb, n, h, w, co = dy.shape
+    ci = x.shape[-1]
+    if tuple(x.shape[:4]) != (nb, n, h, w) or w % 64 or co % 256 or ci % 256 or (n * h * w) % 64:
+        return False
+    if len(dws) != nb or any(d.dtype != torch.float32 or not d.is_contiguous() or tuple(d.shape) != (co, ci, 1, 1)
+                             for d in dws):
+        return False
+    step = co * ci * 4
+    return all(d.data_ptr() == dws[0].data_ptr() + i * step for i, d in enumerate(dws))
+
+
+def conv_wgrad_1x1_batched(dy: torch.Tensor, x: torch.Tensor, dws, *, ws: "WgradWorkspace", beta: float = 0.0,
+                           scale: float = 1.0, dscale: Optional[torch.Tensor] = None) -> None:
+    """dws[b][co,ci,0,0] = scale * [dscale] * sum_m dy[b,m,co] x[b,m,ci]  for b < nb, in ONE GEMM launch
+    (+ nb deterministic slab reductions).  Caller checks wgrad_1x1_batched_ok first."""
+    C = _ext.require()
+    _check_act(dy, "dy")
+    _check_act(x, "x", dtype=dy.dtype)
+    if not wgrad_1x1_batched_ok(dy, x, dws):
+        raise ValueError("batched 1x1 wgrad: unsupported shapes / output layout")
+    nb, n, h, w, co = dy.shape
+    ci = x.shape[-1]
+    m = n * h * w
+    s, mslice, need = wgrad_1x1_batched_plan(m, nb, ci, co)
+    buf = ws.reserve(need)
+    C.conv_wgrad_1x1_batched(dy.data_ptr(), x.data_ptr(), buf.data_ptr(), dws[0].data_ptr(), m, w, ci, co, nb,
+                             m * co, m * ci, co * ci, s, mslice, float(beta), float(scale),
+                             dscale.data_ptr() if dscale is not None else 0, dt_code(dy.dtype),
+                             _ext.stream_ptr(x.device))

@@ -4,9 +4,11 @@ gfx950 kernels (no tracing compiler, no autograd graph of ATen ops).
 Reference math: model/CANNet.py:39-91 (forward), the backward is what
 autograd derives for it in the reference (SURVEY §2.5 kernel inventory).
 
-Data layout: NHWC bf16 activations, fp32 master weights in the model's own
-nn.Parameters, bf16 packed weight copies (forward + flipped dgrad layouts)
-refreshed by one pack kernel per layer whenever the fp32 weights change.
+Data layout: NHWC 16-bit activations (bf16 by default, fp16 optional: one
+element type for every activation / weight pack of the executor), fp32
+master weights in the model's own nn.Parameters, 16-bit packed weight copies
+(forward + flipped dgrad layouts) refreshed by one pack launch whenever the
+fp32 weights change.
 
 Forward (training) saves exactly what the backward needs: every conv input
 (NHWC bf16), the pre-pool activations, the context tables, c_S and w_S.
@@ -56,9 +58,11 @@ class ConvSpec:
 
 
 class CANNetExecutor:
-    def __init__(self, model: nn.Module):
+    def __init__(self, model: nn.Module, dtype: torch.dtype = BF16):
         self.C = _ext.require()
         self.model = model
+        self.act = dtype                   # activation / weight-pack element type
+        self.dt = C.dt_code(dtype)
         params = list(model.parameters())
         pid = {id(p): i for i, p in enumerate(params)}
         self.n_params = len(params)
@@ -110,19 +114,19 @@ class CANNetExecutor:
             w = s.module.weight
             if s.first:
                 # k = tap*4 + c: the pack kernel writes only c < 3, tap < 9 -> pad must be zero
-                fwd = torch.zeros(s.cout, 64, dtype=BF16, device=device)
+                fwd = torch.zeros(s.cout, 64, dtype=self.act, device=device)
                 dgr = None
             else:
-                fwd = torch.empty(s.cout, s.ksize * s.ksize * s.cin, dtype=BF16, device=device)
-                dgr = torch.empty(s.cin, s.ksize * s.ksize * s.cout, dtype=BF16, device=device)
+                fwd = torch.empty(s.cout, s.ksize * s.ksize * s.cin, dtype=self.act, device=device)
+                dgr = torch.empty(s.cin, s.ksize * s.ksize * s.cout, dtype=self.act, device=device)
             self.packs[id(w)] = (fwd, dgr)
         for sc in CONTEXT_SCALES:
             w = self.ctx2[sc].weight
-            self.packs[id(w)] = (torch.empty(512, 512, dtype=BF16, device=device),
-                                 torch.empty(512, 512, dtype=BF16, device=device))
+            self.packs[id(w)] = (torch.empty(512, 512, dtype=self.act, device=device),
+                                 torch.empty(512, 512, dtype=self.act, device=device))
 
     def refresh_packs(self, force: bool = False):
-        """Re-pack bf16 weight copies from the fp32 masters (one launch for all layers)."""
+        """Re-pack the 16-bit weight copies from the fp32 masters (one launch for all layers)."""
         ver = self._weights_version()
         if not force and ver == self._pack_version and self.packs:
             return
@@ -149,7 +153,7 @@ class CANNetExecutor:
         if cur != self._pack_desc_ptrs:
             self._pack_desc = None
             return self.refresh_packs(force=True)
-        self.C.pack_multi(self._pack_desc.data_ptr(), self._pack_desc.shape[0], self._pack_tiles, st)
+        self.C.pack_multi(self._pack_desc.data_ptr(), self._pack_desc.shape[0], self._pack_tiles, self.dt, st)
         self._pack_version = ver
 
     def mark_weights_updated(self):
@@ -173,6 +177,7 @@ class CANNetExecutor:
         for s in self.back:
             need = max(need, self.ws.plan(n * hh * ww, s.cin, s.cout, 3, False)[3])
         need = max(need, self.ws.plan(n * hh * ww, 512, 512, 1, False)[3])
+        need = max(need, C.wgrad_1x1_batched_plan(n * hh * ww, 4, 512, 512)[2])
         self.ws.reserve(need)
         return self.ws
 
@@ -183,12 +188,14 @@ class CANNetExecutor:
 
     def _maxpool(self, x):
         n, h, w, c = x.shape
-        y = torch.empty(n, h // 2, w // 2, c, dtype=BF16, device=x.device)
-        self.C.maxpool_fwd(x.data_ptr(), y.data_ptr(), n, h, w, c, self._stream())
+        y = torch.empty(n, h // 2, w // 2, c, dtype=self.act, device=x.device)
+        self.C.maxpool_fwd(x.data_ptr(), y.data_ptr(), n, h, w, c, self.dt, self._stream())
         return y
 
     def _img(self, img):
-        if img.dim() == 4 and img.shape[-1] == 4 and img.dtype == BF16:
+        if img.dim() == 4 and img.shape[-1] == 4 and img.dtype in C.ACT_DTYPES:
+            if img.dtype != self.act:
+                raise ValueError(f"NHWC4 input is {img.dtype}, the executor computes in {self.act}")
             # already in the first layer's NHWC4 layout (ops/preprocess.py)
             if img.shape[1] % 8 or img.shape[2] % 8:
                 raise ValueError("H, W must be multiples of 8")
@@ -199,8 +206,8 @@ class CANNetExecutor:
         if h % 8 or w % 8:
             raise ValueError(f"H, W must be multiples of 8 (got {h}x{w}); resize as CrowdDataset does")
         img = img.float().contiguous()
-        x4 = torch.empty(n, h, w, 4, dtype=BF16, device=img.device)
-        self.C.img_to_nhwc4(img.data_ptr(), x4.data_ptr(), n, h, w, self._stream())
+        x4 = torch.empty(n, h, w, 4, dtype=self.act, device=img.device)
+        self.C.img_to_nhwc4(img.data_ptr(), x4.data_ptr(), n, h, w, self.dt, self._stream())
         return x4
 
     def forward_features(self, img, save: bool):
@@ -234,20 +241,20 @@ class CANNetExecutor:
         st = self._stream()
         rowacc = torch.empty(n, h, 12, c, dtype=torch.float32, device=fv.device)
         ave = torch.empty(n, 50, c, dtype=torch.float32, device=fv.device)
-        self.C.ctx_reduce(0, fv.data_ptr(), 0, 0, rowacc.data_ptr(), ave.data_ptr(), n, h, w, c, st)
+        self.C.ctx_reduce(0, fv.data_ptr(), 0, 0, rowacc.data_ptr(), ave.data_ptr(), n, h, w, c, self.dt, st)
         table = torch.empty_like(ave)
         for sc in CONTEXT_SCALES:
             o, k = CELL_OFF[sc], sc * sc
             w1 = self.ctx1[sc].weight.detach().view(c, c)
             torch.matmul(ave[:, o:o + k], w1.t(), out=table[:, o:o + k])
-        cs = torch.empty(4, n, h, w, c, dtype=BF16, device=fv.device)
-        self.C.ctx_expand(fv.data_ptr(), table.data_ptr(), cs.data_ptr(), n, h, w, c, st)
-        wts = torch.empty(4, n, h, w, c, dtype=BF16, device=fv.device)
+        cs = torch.empty(4, n, h, w, c, dtype=self.act, device=fv.device)
+        self.C.ctx_expand(fv.data_ptr(), table.data_ptr(), cs.data_ptr(), n, h, w, c, self.dt, st)
+        wts = torch.empty(4, n, h, w, c, dtype=self.act, device=fv.device)
         for i, sc in enumerate(CONTEXT_SCALES):
             fwd, _ = self.packs[id(self.ctx2[sc].weight)]
             C.conv_igemm(cs[i], fwd, None, ksize=1, epi=4, out=wts[i])   # EPI_SIGMOID
-        cat = torch.empty(n, h, w, 2 * c, dtype=BF16, device=fv.device)
-        self.C.ctx_fuse(fv.data_ptr(), wts.data_ptr(), table.data_ptr(), cat.data_ptr(), n, h, w, c, st)
+        cat = torch.empty(n, h, w, 2 * c, dtype=self.act, device=fv.device)
+        self.C.ctx_fuse(fv.data_ptr(), wts.data_ptr(), table.data_ptr(), cat.data_ptr(), n, h, w, c, self.dt, st)
         saved = dict(ave=ave, table=table, cs=cs, wts=wts, rowacc=rowacc) if save else None
         return cat, saved
 
@@ -255,7 +262,7 @@ class CANNetExecutor:
         n, h, w, _ = b6.shape
         et = torch.empty(n, 1, h, w, dtype=torch.float32, device=b6.device)
         self.C.head_fwd(b6.data_ptr(), self.head.weight.detach().data_ptr(), self.head.bias.detach().data_ptr(),
-                        et.data_ptr(), n * h * w, self._stream())
+                        et.data_ptr(), n * h * w, self.dt, self._stream())
         return et
 
     @torch.no_grad()
@@ -266,11 +273,13 @@ class CANNetExecutor:
     # ----------------------------------------------------------- backward
     def backward_features(self, sv, d_b6: torch.Tensor, grads: Sequence[Optional[torch.Tensor]],
                           on_grad_ready: Optional[Callable[[List[int]], None]] = None, beta: float = 0.0,
-                          scale: float = 1.0):
+                          scale: float = 1.0, dscale: Optional[torch.Tensor] = None):
         """d_b6: grad wrt the PRE-activation of the last backend conv (ReLU already applied).
 
         grads[i] is the fp32 output tensor for model.parameters()[i] (written, or
         accumulated when beta=1).  Entries for the head must already be filled.
+        dscale: optional fp32 device scalar multiplied into every weight gradient
+        (1 / loss scale when d_b6 carries a loss scale, fp16 step).
         """
         st = self._stream()
         ws = self.ws or self.workspace(*self._shape_from(sv))
@@ -278,7 +287,7 @@ class CANNetExecutor:
 
         def wg(spec_or_w, dy, x, ksize, dil, first, wi, bi):
             C.conv_wgrad(dy, x, grads[wi], grads[bi] if bi is not None else None, ksize=ksize, dil=dil, first=first,
-                         ws=ws, beta=beta, scale=scale)
+                         ws=ws, beta=beta, scale=scale, dscale=dscale)
             ready([wi] + ([bi] if bi is not None else []))
 
         # ---- backend, reverse
@@ -292,7 +301,7 @@ class CANNetExecutor:
             else:
                 dcat = C.conv_igemm(dy, dgr, None, ksize=3, dil=s.dil, epi=C.EPI_NONE)
         # ---- context module
-        dy = self._context_bwd(sv["ctx"], sv["fv"], dcat, grads, ws, beta, scale, ready)
+        dy = self._context_bwd(sv["ctx"], sv["fv"], dcat, grads, ws, beta, scale, ready, dscale)
         # ---- frontend, reverse
         for s in reversed(self.front):
             x = sv["front_in"][s.idx]
@@ -306,29 +315,36 @@ class CANNetExecutor:
                 full = sv["pre_pool"][prev.idx]
                 dfull = torch.empty_like(full)
                 nn_, hh, ww, cc = full.shape
-                self.C.maxpool_bwd_relu(full.data_ptr(), dp.data_ptr(), dfull.data_ptr(), nn_, hh, ww, cc, st)
+                self.C.maxpool_bwd_relu(full.data_ptr(), dp.data_ptr(), dfull.data_ptr(), nn_, hh, ww, cc, self.dt,
+                                        st)
                 dy = dfull
             else:
                 dy = C.conv_igemm(dy, dgr, None, ksize=3, dil=1, epi=C.EPI_MASK, mask=x)
 
-    def _context_bwd(self, ctx, fv, dcat, grads, ws, beta, scale, ready):
+    def _context_bwd(self, ctx, fv, dcat, grads, ws, beta, scale, ready, dscale=None):
         """Backward of the context module; returns d(F10 pre-activation) (ReLU mask of fv applied)."""
         st = self._stream()
         n, h, w, c = fv.shape
-        dz = torch.empty(4, n, h, w, c, dtype=BF16, device=fv.device)
+        dz = torch.empty(4, n, h, w, c, dtype=self.act, device=fv.device)
         sdir = torch.empty_like(dz)
         self.C.ctx_bwd_e1(dcat.data_ptr(), ctx["wts"].data_ptr(), ctx["table"].data_ptr(), dz.data_ptr(),
-                          sdir.data_ptr(), n, h, w, c, st)
+                          sdir.data_ptr(), n, h, w, c, self.dt, st)
         dc = torch.empty_like(dz)
         for i, sc in enumerate(CONTEXT_SCALES):
             _, dgr = self.packs[id(self.ctx2[sc].weight)]
             C.conv_igemm(dz[i], dgr, None, ksize=1, epi=C.EPI_NONE, out=dc[i])
-            wi = self.ctx2_index[sc]
-            C.conv_wgrad(dz[i], ctx["cs"][i], grads[wi], None, ksize=1, ws=ws, beta=beta, scale=scale)
+        # the four conv{S}_2 weight gradients: one batched GEMM when their arena slots are adjacent
+        dws = [grads[self.ctx2_index[sc]] for sc in CONTEXT_SCALES]
+        if C.wgrad_1x1_batched_ok(dz, ctx["cs"], dws):
+            C.conv_wgrad_1x1_batched(dz, ctx["cs"], dws, ws=ws, beta=beta, scale=scale, dscale=dscale)
+        else:
+            for i, sc in enumerate(CONTEXT_SCALES):
+                C.conv_wgrad(dz[i], ctx["cs"][i], dws[i], None, ksize=1, ws=ws, beta=beta, scale=scale, dscale=dscale)
         ready([self.ctx2_index[sc] for sc in CONTEXT_SCALES])
         rowacc = ctx["rowacc"]
         dA = torch.empty(n, 50, c, dtype=torch.float32, device=fv.device)
-        self.C.ctx_reduce(1, 0, sdir.data_ptr(), dc.data_ptr(), rowacc.data_ptr(), dA.data_ptr(), n, h, w, c, st)
+        self.C.ctx_reduce(1, 0, sdir.data_ptr(), dc.data_ptr(), rowacc.data_ptr(), dA.data_ptr(), n, h, w, c, self.dt,
+                          st)
         dave = torch.empty_like(dA)
         ave = ctx["ave"]
         for sc in CONTEXT_SCALES:
@@ -339,15 +355,17 @@ class CANNetExecutor:
             gw = gA.t() @ ave[:, o:o + k].reshape(-1, c)
             if scale != 1.0:
                 gw = gw * scale
+            if dscale is not None:
+                gw = gw * dscale
             if beta:
                 g.add_(gw)
             else:
                 g.copy_(gw)
             torch.matmul(dA[:, o:o + k], w1, out=dave[:, o:o + k])
         ready([self.ctx1_index[sc] for sc in CONTEXT_SCALES])
-        dfv = torch.empty(n, h, w, c, dtype=BF16, device=fv.device)
+        dfv = torch.empty(n, h, w, c, dtype=self.act, device=fv.device)
         self.C.ctx_bwd_final(dcat.data_ptr(), dc.data_ptr(), dave.data_ptr(), fv.data_ptr(), dfv.data_ptr(), n, h, w,
-                             c, st)
+                             c, self.dt, st)
         return dfv
 
     @staticmethod
@@ -358,13 +376,15 @@ class CANNetExecutor:
     @staticmethod
     def input_hw(img):
         """(N, H, W) of an NCHW image batch or an NHWC4 prepacked batch."""
-        if img.dim() == 4 and img.shape[-1] == 4 and img.dtype == BF16:
+        if img.dim() == 4 and img.shape[-1] == 4 and img.dtype in C.ACT_DTYPES:
             return img.shape[0], img.shape[1], img.shape[2]
         return img.shape[0], img.shape[2], img.shape[3]
 
     # ----------------------------------------------------------- training head
-    def head_train(self, b6, gt, grads, gscale: float = 1.0, beta: float = 0.0):
-        """Fused: et, MSE(sum) loss, d(et), d(b6 pre-act) (ReLU-masked), head grads. Returns (loss, et, d_b6)."""
+    def head_train(self, b6, gt, grads, gscale: float = 1.0, beta: float = 0.0,
+                   lscale: Optional[torch.Tensor] = None):
+        """Fused: et, MSE(sum) loss, d(et), d(b6 pre-act) (ReLU-masked), head grads. Returns (loss, et, d_b6).
+        lscale: optional fp32 device scalar (loss scale) applied to d_b6 only; head grads stay unscaled."""
         n, h, w, c = b6.shape
         if tuple(gt.shape) != (n, 1, h, w):
             raise ValueError(f"gt shape {tuple(gt.shape)} != {(n, 1, h, w)}")
@@ -378,7 +398,8 @@ class CANNetExecutor:
         self.C.head_train(b6.data_ptr(), self.head.weight.detach().data_ptr(), self.head.bias.detach().data_ptr(),
                           gt.data_ptr(), et.data_ptr(), d_b6.data_ptr(), part.data_ptr(), nblk,
                           grads[self.head_w_index].data_ptr(), grads[self.head_b_index].data_ptr(), loss.data_ptr(),
-                          P, float(gscale), float(beta), self._stream())
+                          P, float(gscale), float(beta), lscale.data_ptr() if lscale is not None else 0, self.dt,
+                          self._stream())
         return loss, et, d_b6
 
     # ----------------------------------------------------------- autograd entry
@@ -408,7 +429,7 @@ class _CANNetFn(torch.autograd.Function):
         g = g_et.float().reshape(n, h, w, 1)
         b6f = b6.float()
         hw = ex.head.weight.detach().view(1, c)
-        d_b6 = (g * hw * (b6f > 0)).to(BF16).contiguous()
+        d_b6 = (g * hw * (b6f > 0)).to(ex.act).contiguous()
         grads[ex.head_w_index].copy_((g * b6f).sum(dim=(0, 1, 2)).view_as(params[ex.head_w_index]))
         grads[ex.head_b_index].copy_(g.sum().view(1))
         ex.workspace(*CANNetExecutor._shape_from(ctx.sv))

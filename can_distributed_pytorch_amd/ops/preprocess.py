@@ -14,9 +14,9 @@ from . import _ext
 
 
 def preprocess_batch(images: Sequence[torch.Tensor], densities: Sequence[torch.Tensor], flips: Sequence[bool],
-                     device, downsample: int = 8) -> Tuple[torch.Tensor, torch.Tensor]:
+                     device, downsample: int = 8, dtype: torch.dtype = torch.bfloat16) -> Tuple[torch.Tensor, torch.Tensor]:
     """images: uint8 [H,W] / [H,W,C] (CPU or GPU), densities: fp32 [H,W].  All samples must
-    resize to the same (H//d*d, W//d*d).  Returns (x4 [N,Ho,Wo,4] bf16, gt [N,1,Ho/d,Wo/d] fp32)."""
+    resize to the same (H//d*d, W//d*d).  Returns (x4 [N,Ho,Wo,4] bf16/fp16, gt [N,1,Ho/d,Wo/d] fp32)."""
     C = _ext.require()
     dev = torch.device(device)
     n = len(images)
@@ -24,7 +24,9 @@ def preprocess_batch(images: Sequence[torch.Tensor], densities: Sequence[torch.T
         raise ValueError("images, densities and flips must have the same non-zero length")
     h0, w0 = images[0].shape[:2]
     ho, wo = (h0 // downsample) * downsample, (w0 // downsample) * downsample
-    x4 = torch.empty(n, ho, wo, 4, dtype=torch.bfloat16, device=dev)
+    from .conv import dt_code
+    dt = dt_code(dtype)
+    x4 = torch.empty(n, ho, wo, 4, dtype=dtype, device=dev)
     gt = torch.empty(n, 1, ho // downsample, wo // downsample, dtype=torch.float32, device=dev)
     st = _ext.stream_ptr(dev)
     for i, (im, dm, fl) in enumerate(zip(images, densities, flips)):
@@ -38,7 +40,7 @@ def preprocess_batch(images: Sequence[torch.Tensor], densities: Sequence[torch.T
         dm = dm.to(dev, dtype=torch.float32, non_blocking=True).contiguous()
         if tuple(dm.shape) != (hh, ww):
             raise ValueError("density must match the image size")
-        C.preprocess_image(im.data_ptr(), hh, ww, ch, int(bool(fl)), x4[i].data_ptr(), ho, wo, st)
+        C.preprocess_image(im.data_ptr(), hh, ww, ch, int(bool(fl)), x4[i].data_ptr(), ho, wo, dt, st)
         C.preprocess_density(dm.data_ptr(), hh, ww, int(bool(fl)), gt[i].data_ptr(), ho // downsample,
                              wo // downsample, float(downsample * downsample), st)
     return x4, gt

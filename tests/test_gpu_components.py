@@ -18,7 +18,7 @@ def test_maxpool_fwd_bwd():
     n, h, w, c = 2, 12, 20, 64
     x = torch.relu(torch.randn(n, h, w, c, device="cuda")).to(BF16)
     y = torch.empty(n, h // 2, w // 2, c, dtype=BF16, device="cuda")
-    C.maxpool_fwd(x.data_ptr(), y.data_ptr(), n, h, w, c, _ext.stream_ptr())
+    C.maxpool_fwd(x.data_ptr(), y.data_ptr(), n, h, w, c, 0, _ext.stream_ptr())
     xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
     yr = F.max_pool2d(xr, 2, 2)
     assert torch.equal(y.float(), yr.detach().permute(0, 2, 3, 1))
@@ -26,7 +26,7 @@ def test_maxpool_fwd_bwd():
     (gx,) = torch.autograd.grad(yr, xr, g.float().permute(0, 3, 1, 2))
     ref = gx.permute(0, 2, 3, 1) * (x.float() > 0)
     dx = torch.empty_like(x)
-    C.maxpool_bwd_relu(x.data_ptr(), g.data_ptr(), dx.data_ptr(), n, h, w, c, _ext.stream_ptr())
+    C.maxpool_bwd_relu(x.data_ptr(), g.data_ptr(), dx.data_ptr(), n, h, w, c, 0, _ext.stream_ptr())
     torch.cuda.synchronize()
     assert torch.equal(dx.float(), ref)
 

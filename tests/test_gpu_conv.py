@@ -164,3 +164,21 @@ def test_conv_wgrad_halo_path(n, h, w, ci, co):
     gw, gb = torch.autograd.grad(y, (wr, br), dy.float().permute(0, 3, 1, 2))
     _close(dw, gw, 1e-2)
     _close(db, gb, 1e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_conv_wgrad_1x1_batched(dtype):
+    """The four context-module 1x1 weight gradients in one batched launch == fp32 reference, per item."""
+    from can_distributed_pytorch_amd.ops import conv as C
+    torch.manual_seed(7)
+    nb, n, h, w, c = 4, 2, 12, 128, 512
+    dy = torch.randn(nb, n, h, w, c, device="cuda").to(dtype)
+    x = torch.randn(nb, n, h, w, c, device="cuda").to(dtype)
+    arena = torch.full((nb * c * c,), float("nan"), device="cuda")
+    dws = [arena[i * c * c:(i + 1) * c * c].view(c, c, 1, 1) for i in range(nb)]
+    assert C.wgrad_1x1_batched_ok(dy, x, dws)
+    ws = C.WgradWorkspace("cuda")
+    C.conv_wgrad_1x1_batched(dy, x, dws, ws=ws, scale=0.5)
+    for b in range(nb):
+        ref = 0.5 * dy[b].float().reshape(-1, c).t() @ x[b].float().reshape(-1, c)
+        _close(dws[b].view(c, c), ref, 1e-2)

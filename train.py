@@ -119,6 +119,9 @@ def main(args):
     if args.impl == "hip" and not use_gpu:
         print("[no GPU: falling back to --impl torch on CPU]")
         args.impl = "torch"
+    if args.impl == "hip" and args.dtype == "fp32":
+        print("[--dtype fp32: the native kernels compute in bf16/fp16; using --impl torch]")
+        args.impl = "torch"
     if args.batch_norm and args.impl == "hip":
         print("[--batch-norm: the fused native step has no BN layers; using --impl torch]")
         args.impl = "torch"
@@ -135,7 +138,8 @@ def main(args):
     prep = None
     if raw:
         from can_distributed_pytorch_amd.ops.preprocess import preprocess_batch
-        prep = lambda b: preprocess_batch(b[0], b[1], b[2], device)  # noqa: E731
+        act = torch.float16 if args.dtype == "fp16" else torch.bfloat16
+        prep = lambda b: preprocess_batch(b[0], b[1], b[2], device, dtype=act)  # noqa: E731
 
     model = CANNet(vgg16_path=args.vgg16 or None, backend="hip" if args.impl == "hip" else "torch",
                    batch_norm=args.batch_norm)
@@ -150,7 +154,7 @@ def main(args):
     fixed = bool(args.synthetic)
     graph = args.graph if args.graph is not None else (fixed and world == 1)
     if args.impl == "hip":
-        stepper = build_trainer(impl="hip", dtype="bf16", device=device, world=world, lr=base_lr, graph=graph,
+        stepper = build_trainer(impl="hip", dtype=args.dtype, device=device, world=world, lr=base_lr, graph=graph,
                                 model=model)
         net = stepper.model
         momentum = stepper.mom
