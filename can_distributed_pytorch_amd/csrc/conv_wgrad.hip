@@ -557,7 +557,7 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
   constexpr int NIA = A_BYTES / 1024, NIB = B_BYTES / 1024;
   constexpr int GA = NIA / NW, GB = NIB / NW;
   static_assert(NIA % NW == 0 && NIB % NW == 0, "instruction split");
-  static_assert(RBB == 512, "B row = 256 k (2 rows per 1-KiB DMA)");
+  static_assert(RBB == 512 || RBB == 256, "B row = 256 or 128 k (2 or 4 pixel rows per 1-KiB DMA)");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -595,12 +595,12 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
     dw = (tap - kh * 3 - 1) * a.dil;
   }
   const int ci0 = k0 - tap * a.Cin;
-  const int lrow = lane >> 5;
-  int boff[GB];
+  int boff[GB], brow[GB];
 #pragma unroll
   for (int j = 0; j < GB; ++j) {
     const int byte = (wave + NW * j) * 1024 + lane * 16;
     const int row = byte / RBB;
+    brow[j] = row;
     const int lc16 = swz8b<RBB>(row, ((byte % RBB) / 16) * 2) >> 1;
     boff[j] = (row + dh * a.W + dw) * a.Cin + ci0 + lc16 * 8;
   }
@@ -620,7 +620,7 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
     const bf16_t* xs = gx + (size_t)m0 * a.Cin;
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
-      const int iw = ow0 + dw + 2 * (wave + NW * j) + lrow;
+      const int iw = ow0 + dw + brow[j];
       const bool ok = row_ok && ((unsigned)iw < (unsigned)a.W);
       const void* src = ok ? (const void*)(xs + boff[j]) : (const void*)a.zero;
       __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sbase + A_BYTES + (wave + NW * j) * 1024), 16, 0, 0);
@@ -1087,6 +1087,8 @@ static void wgrad_tile(int cfg, int* TCo, int* TK, int* BKM) {
     case 6: *TCo = 128; *TK = 256; *BKM = 64; break;
     case 7: *TCo = 256; *TK = 256; *BKM = 64; break;
     case 9: *TCo = 256; *TK = 256; *BKM = 64; break;   // v2 (row-aligned layers), falls back to 7
+    case 10: *TCo = 256; *TK = 128; *BKM = 64; break;  // v2 256co x 128k (Cin = 128), falls back to 2
+    case 11: *TCo = 128; *TK = 256; *BKM = 64; break;  // v2 128co x 256k (Cout = 128), falls back to 6
     case 8: *TCo = 0; *TK = 0; *BKM = 128; break;   // halo kernel: tiles of 2x64 pixels
     default: *TCo = 64; *TK = 64; *BKM = 128; break;
   }
@@ -1101,7 +1103,8 @@ extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, in
   if (first) cfg = 0;
   else if (halo_ok && getenv("CANNET_NO_HALO") == nullptr && M >= 262144) cfg = 8;
   else if (Cout % 256 == 0 && K >= 2048) cfg = (K % 256 == 0 && getenv("CANNET_WGRAD_V1") == nullptr) ? 9 : 7;
-  else if (Cout % 256 == 0 && K >= 1024) cfg = 2;
+  else if (Cout % 256 == 0 && K >= 1024) cfg = (Cin % 128 == 0 && getenv("CANNET_WGRAD_V1") == nullptr) ? 10 : 2;
+  else if (Cout == 128 && Cin % 256 == 0 && K >= 2048 && getenv("CANNET_WGRAD_V1") == nullptr) cfg = 11;
   else if (Cout % 128 == 0 && K >= 2048) cfg = 6;
   else if (Cout % 128 == 0) cfg = 1;
   else if (K >= 128) cfg = 3;
@@ -1217,6 +1220,24 @@ static int conv_wgrad_impl(const void* dy, const void* x, float* ws, float* wsb,
         } else
           rc = launch_wgrad2<DT, 4, 2, 1, 2, 2, 2>(a, s);   // same tiles / slicing as cfg 7
         break;
+      case 10:   // 256co x 128k v2 (k tile = one tap of a Cin % 128 layer); fallback = cfg 2 tiles
+      case 11: { // 128co x 256k v2 (Cout = 128); fallback = cfg 6 tiles
+        const int tk = (cfg == 10) ? 128 : 256;
+        if (Cout % (cfg == 10 ? 256 : 128)) return -4;
+        if (W % 64 == 0 && Cin % tk == 0 && K % tk == 0 && mslice % 64 == 0 &&
+            (long long)a.M * Cout * 2 < 0x7fffffffLL && Cout <= 2048) {
+          if (wsb_used) {
+            Sb = kBiasParts;
+            hipLaunchKernelGGL(bias_colsum_kernel<DT>, dim3(Sb), dim3(256), 0, s, a.dy, wsb_used, a.M, Cout, Sb);
+          }
+          WgradArgs2 g = a;
+          g.wsb = nullptr;
+          rc = (cfg == 10) ? launch_wgrad3<DT, 4, 2, 1>(g, s) : launch_wgrad3<DT, 2, 4, 1>(g, s);
+        } else {
+          rc = (cfg == 10) ? launch_wgrad2<DT, 4, 2, 1, 3, 1, 2>(a, s) : launch_wgrad2<DT, 2, 2, 1, 3, 2, 2>(a, s);
+        }
+        break;
+      }
       default: return -5;
     }
   }

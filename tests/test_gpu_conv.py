@@ -182,3 +182,26 @@ def test_conv_wgrad_1x1_batched(dtype):
     for b in range(nb):
         ref = 0.5 * dy[b].float().reshape(-1, c).t() @ x[b].float().reshape(-1, c)
         _close(dws[b].view(c, c), ref, 1e-2)
+
+
+@pytest.mark.parametrize("n,h,w,ci,co,dil,cfg,bias", [
+    (1, 6, 64, 128, 256, 1, 10, True), (2, 5, 128, 128, 512, 2, 10, False), (1, 9, 64, 256, 128, 2, 11, True),
+    (2, 4, 64, 512, 128, 1, 11, True)])
+def test_conv_wgrad_v2_half_tiles(n, h, w, ci, co, dil, cfg, bias):
+    """v2 pipelined wgrad with 256co x 128k (Cin = 128, cfg 10) and 128co x 256k (Cout = 128, cfg 11) tiles."""
+    from can_distributed_pytorch_amd.ops import _ext
+    from can_distributed_pytorch_amd.ops import conv as C
+    assert _ext.require().wgrad_plan(n * h * w, ci, co, 3, 0, 1024)[2] == cfg
+    torch.manual_seed(8)
+    x = torch.randn(n, h, w, ci, device="cuda").to(torch.bfloat16)
+    dy = torch.randn(n, h, w, co, device="cuda").to(torch.bfloat16)
+    dw = torch.empty(co, ci, 3, 3, device="cuda")
+    db = torch.empty(co, device="cuda") if bias else None
+    C.conv_wgrad(dy, x, dw, db, ksize=3, dil=dil)
+    wr = torch.zeros(co, ci, 3, 3, device="cuda", requires_grad=True)
+    br = torch.zeros(co, device="cuda", requires_grad=True)
+    y = F.conv2d(x.float().permute(0, 3, 1, 2), wr, br, padding=dil, dilation=dil)
+    gw, gb = torch.autograd.grad(y, (wr, br), dy.float().permute(0, 3, 1, 2))
+    _close(dw, gw, 1e-2)
+    if bias:
+        _close(db, gb, 1e-2)
