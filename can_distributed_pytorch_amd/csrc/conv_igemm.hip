@@ -543,9 +543,17 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
     sh += i_c0;
     const int i_k = i_tap * a.Cin + i_c0;
     unsigned char* sbase = smem + buf * STAGE;
+#if defined(CAN_PROBE) && CAN_PROBE >= 2
+    if (++i_tap == ntap) { i_tap = 0; i_c0 += 64; }
+    return;
+#endif
 #pragma unroll
     for (int j = 0; j < GA; ++j)
       __builtin_amdgcn_global_load_lds((const void*)(a.w + aoff[j] + i_k), (__attribute__((address_space(3))) void*)(sbase + (wave + NW * j) * 1024), 16, 0, 0);
+#if defined(CAN_PROBE) && CAN_PROBE == 1
+    if (++i_tap == ntap) { i_tap = 0; i_c0 += 64; }
+    return;
+#endif
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
       const void* src = ((bmask[j] >> i_tap) & 1u) ? (const void*)(a.x + boff[j] + sh) : (const void*)a.zero;
@@ -565,6 +573,11 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
     const uint4* As = reinterpret_cast<const uint4*>(smem + buf * STAGE);
     const uint4* Bs = reinterpret_cast<const uint4*>(smem + buf * STAGE + A_BYTES);
     const int chunk = kk * 4 + fq;
+#if defined(CAN_PROBE) && CAN_PROBE >= 3
+    for (int j = 0; j < 4; ++j) af[j] = __builtin_bit_cast(frag8_t, make_uint4(buf + lane, kk, j, 1));
+    for (int i = 0; i < 4 * PW; ++i) bfr[i] = __builtin_bit_cast(frag8_t, make_uint4(buf, kk + lane, i, 1));
+    return;
+#endif
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int row = wc * 64 + j * 16 + fr;
