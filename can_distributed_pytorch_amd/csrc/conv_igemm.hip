@@ -675,16 +675,22 @@ struct HaloConvArgs {
   int N, H, W, tiles_x, tiles_y;
 };
 
-template <int DT, int CO, int EPI>
-__global__ void __launch_bounds__(512, 1) conv_halo64_kernel(HaloConvArgs a) {
-  constexpr int TR = 4, TCOL = 128, HR = TR + 2, HC = TCOL + 2;
-  constexpr int HPIX = HR * HC;                       // 780 halo pixels
+// TCOL = 64 (CO = 64 only): 4 waves, one per output row, 75 KB of LDS, so TWO
+// blocks share a CU and one block's halo fetch overlaps the other's MFMAs (the
+// 128-column block is alone on its CU: fetch, then compute, then store).
+template <int DT, int CO, int EPI, int TCOL>
+__global__ void __launch_bounds__((CO == 64 && TCOL == 64) ? 256 : 512, (TCOL == 64) ? 2 : 1)
+conv_halo64_kernel(HaloConvArgs a) {
+  constexpr int TR = 4, HR = TR + 2, HC = TCOL + 2;
+  constexpr int NW = (CO == 64 && TCOL == 64) ? 4 : 8; // waves
+  constexpr int HPIX = HR * HC;                       // 780 halo pixels (TCOL 128)
   constexpr int NHI = (HPIX + 7) / 8;                 // 98 one-KiB DMA pieces
   constexpr int HALO_BYTES = NHI * 1024;
   constexpr int WTAP = CO * 128;                      // one tap of weights: CO rows x 64 ci
-  constexpr int GW = WTAP / 1024 / 8;                 // weight DMA pieces per wave per tap
+  constexpr int GW = WTAP / 1024 / NW;                // weight DMA pieces per wave per tap
   constexpr int PW = CO / 64;                         // pixel fragments per wave / 4
   static_assert(GW >= 1, "weights split");
+  static_assert(TCOL == 128 || (TCOL == 64 && CO == 64), "tile");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* halo = smem;
@@ -700,7 +706,7 @@ __global__ void __launch_bounds__(512, 1) conv_halo64_kernel(HaloConvArgs a) {
   const int oh0 = ty * TR, ow0 = tx * TCOL;
 
   // ---- halo DMA (once): piece i covers halo pixels 8i..8i+7
-  for (int i = wave; i < NHI; i += 8) {
+  for (int i = wave; i < NHI; i += NW) {
     const int hp = i * 8 + (lane >> 3);
     const int hr = hp / HC, hc = hp - hr * HC;
     const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
@@ -713,19 +719,19 @@ __global__ void __launch_bounds__(512, 1) conv_halo64_kernel(HaloConvArgs a) {
     unsigned char* dst = wring + (t % 3) * WTAP;
 #pragma unroll
     for (int j = 0; j < GW; ++j) {
-      const int r = (wave + 8 * j) * 8 + (lane >> 3);
+      const int r = (wave + NW * j) * 8 + (lane >> 3);
       const int lc = (lane & 7) ^ (r & 7);
       __builtin_amdgcn_global_load_lds((const void*)(a.w + (size_t)perm_row(r) * 576 + t * 64 + lc * 8),
-                                       (__attribute__((address_space(3))) void*)(dst + (wave + 8 * j) * 1024), 16, 0, 0);
+                                       (__attribute__((address_space(3))) void*)(dst + (wave + NW * j) * 1024), 16, 0, 0);
     }
   };
   issue_w(0);
   issue_w(1);
 
   // wave -> (row, co half / column half)
-  const int r = wave >> 1;
+  const int r = (NW == 4) ? wave : (wave >> 1);
   const int wc = (CO == 128) ? (wave & 1) : 0;
-  const int colbase = (CO == 128) ? 0 : (wave & 1) * 64;
+  const int colbase = (CO == 128 || NW == 4) ? 0 : (wave & 1) * 64;
   f32x4 acc[4][4 * PW];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
@@ -912,17 +918,18 @@ __global__ void __launch_bounds__(512) conv_first_halo_kernel(HaloConvArgs a) {
   }
 }
 
-template <int DT, int CO, int EPI>
+template <int DT, int CO, int EPI, int TCOL>
 static int launch_halo64(const HaloConvArgs& a, hipStream_t s) {
-  constexpr int HALO_BYTES = ((6 * 130 + 7) / 8) * 1024;
+  constexpr int HALO_BYTES = ((6 * (TCOL + 2) + 7) / 8) * 1024;
+  constexpr int NW = (CO == 64 && TCOL == 64) ? 4 : 8;
   const size_t lds = HALO_BYTES + 3 * (size_t)CO * 128;
-  auto kfn = conv_halo64_kernel<DT, CO, EPI>;
+  auto kfn = conv_halo64_kernel<DT, CO, EPI, TCOL>;
   static bool attr = false;
   if (!attr) {
     CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
-  hipLaunchKernelGGL(kfn, dim3(a.N * a.tiles_y * a.tiles_x), dim3(512), lds, s, a);
+  hipLaunchKernelGGL(kfn, dim3(a.N * a.tiles_y * a.tiles_x), dim3(64 * NW), lds, s, a);
   return (int)hipGetLastError();
 }
 
@@ -1003,9 +1010,12 @@ static int conv_igemm_impl(const void* x, const void* w, const float* bias, cons
     HaloConvArgs h;
     h.x = a.x; h.w = a.w; h.bias = a.bias; h.mask = a.mask; h.y = a.y; h.zero = conv_zero_page();
     if (!h.zero) return -10;
-    h.N = N; h.H = H; h.W = W; h.tiles_x = (W + 127) / 128; h.tiles_y = (H + 3) / 4;
+    // Cout = 64: 64-column tiles, two blocks per CU (CANNET_HALO_TCOL128 = the 128-column tiles)
+    const bool narrow = Cout == 64 && getenv("CANNET_HALO_TCOL128") == nullptr;
+    h.N = N; h.H = H; h.W = W; h.tiles_x = narrow ? (W + 63) / 64 : (W + 127) / 128; h.tiles_y = (H + 3) / 4;
 #define CAN_HALO_CASE(E) \
-    if (epi == E) return (Cout == 64) ? launch_halo64<DT, 64, E>(h, s) : launch_halo64<DT, 128, E>(h, s);
+    if (epi == E) return (Cout == 128) ? launch_halo64<DT, 128, E, 128>(h, s) \
+                         : narrow ? launch_halo64<DT, 64, E, 64>(h, s) : launch_halo64<DT, 64, E, 128>(h, s);
     CAN_HALO_CASE(EPI_BIAS_RELU)
     CAN_HALO_CASE(EPI_MASK)
     CAN_HALO_CASE(EPI_NONE)

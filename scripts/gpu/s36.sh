@@ -1,0 +1,10 @@
+#!/bin/bash
+# halo wgrad v2 (8-wave ci split) vs v1 (9 waves, one per tap): numerics + per-layer + step, same box
+cd "$GRAFT_REPO_ROOT" || exit 2
+S=scripts/gpu/run_step.sh
+$S conv_tests 600 python -u -m pytest tests/test_gpu_conv.py tests/test_gpu_fp16.py -x -q -rf --timeout 240 --timeout-method thread || exit $?
+$S convs_new 300 python scripts/bench_convs.py --no-ref --layers F2,F3,F4 || exit $?
+CANNET_WGRAD_HALO1=1 $S convs_old 300 python scripts/bench_convs.py --no-ref --layers F2,F3,F4 || exit $?
+$S bench_new 600 python bench.py --steps 30 --warmup 5 || exit $?
+CANNET_WGRAD_HALO1=1 $S bench_old 600 python bench.py --steps 30 --warmup 5 || exit $?
+echo done
