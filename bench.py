@@ -44,9 +44,11 @@ def parse():
     p.add_argument("--width", type=int, default=1024)
     p.add_argument("--impl", choices=["hip", "torch"], default=os.environ.get("CANNET_BENCH_IMPL", "hip"))
     p.add_argument("--dtype", choices=["bf16", "fp32", "fp16"], default="bf16")
-    p.add_argument("--graph", type=int, default=-1,
-                   help="hipGraph-capture the step (hip impl); default: on for 1 GPU, off for N>1 (no measurable "
-                        "gain at ~30 ms/step, and eager RCCL launches are the lower-risk path)")
+    p.add_argument("--graph", type=int, default=0,
+                   help="hipGraph-capture the step (hip impl).  Off by default: the ROCm graph executes its nodes "
+                        "in order, so the weight-gradient side stream (which overlaps the data-gradient chain) "
+                        "only pays off eagerly (404 vs 390 img/s on 1 GPU, same-box A/B), and ~140 launches per "
+                        "20 ms step cost nothing")
     p.add_argument("--profile-steps", type=int, default=0)
     return p.parse_args()
 
@@ -67,8 +69,6 @@ def main():
     from can_distributed_pytorch_amd.data.synthetic import make_synthetic_batch, expected_flops_per_image
 
     torch.manual_seed(0)
-    if a.graph < 0:
-        a.graph = 1 if world == 1 else 0
     trainer = build_trainer(impl=a.impl, dtype=a.dtype, device=dev, world=world, lr=1e-7,
                             batch=a.batch, height=a.height, width=a.width, graph=bool(a.graph))
     # a small pool of distinct synthetic batches, resident on the GPU

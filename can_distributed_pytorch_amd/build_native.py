@@ -5,6 +5,14 @@ Every ``csrc/*.hip`` translation unit (kernels, no torch headers) and
 an object under ``build/`` and linked into
 ``can_distributed_pytorch_amd/_C.<abi>.so``.  Objects are rebuilt only when a
 source or header is newer.  Usage: ``python -m can_distributed_pytorch_amd.build_native [-j N]``.
+
+``--asan`` builds the host-AddressSanitizer variant ``_C_asan`` (SURVEY §5 race
+detection / sanitizers): the host C++ of the runtime (pybind bindings, RCCL
+communicator, bucketed reducer) and the host side of every .hip translation
+unit (launch stubs, planning code) compiled with ``-fsanitize=address``; GPU
+code is NOT instrumented (``-Xarch_host``: device ASan is not available on this
+pool).  Load it with ``CANNET_ASAN=1`` under the ASan runtime, see
+``asan_env()`` / ``scripts/asan_check.sh``.
 """
 from __future__ import annotations
 
@@ -24,9 +32,25 @@ HIPCC = os.path.join(ROCM, "bin", "hipcc")
 ARCH = os.environ.get("CANNET_OFFLOAD_ARCH", "gfx950")
 
 
-def ext_path() -> str:
+def ext_path(asan: bool = False) -> str:
     suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
-    return os.path.join(PKG, "_C" + suffix)
+    return os.path.join(PKG, ("_C_asan" if asan else "_C") + suffix)
+
+
+def asan_runtime() -> str:
+    """Path of the clang ASan runtime matching hipcc (to LD_PRELOAD before python)."""
+    r = subprocess.run([HIPCC, "-print-file-name=libclang_rt.asan-x86_64.so"], capture_output=True, text=True)
+    return r.stdout.strip()
+
+
+def asan_env(base=None) -> dict:
+    """Environment for a child python that imports the ASan build (_C_asan)."""
+    env = dict(os.environ if base is None else base)
+    env["LD_PRELOAD"] = asan_runtime() + ((":" + env["LD_PRELOAD"]) if env.get("LD_PRELOAD") else "")
+    # python itself is not instrumented: no leak report for the interpreter, runtime may not be first
+    env["ASAN_OPTIONS"] = "detect_leaks=0:verify_asan_link_order=0:halt_on_error=1:abort_on_error=1"
+    env["CANNET_ASAN"] = "1"
+    return env
 
 
 def _newer(src_files, target) -> bool:
@@ -36,18 +60,26 @@ def _newer(src_files, target) -> bool:
     return any(os.path.getmtime(f) > t for f in src_files)
 
 
-def _compile(src: str, headers, verbose=False) -> str:
+ASAN_HOST = ["-fsanitize=address", "-fno-omit-frame-pointer", "-g"]
+
+
+def _compile(src: str, headers, verbose=False, asan: bool = False) -> str:
     import pybind11
-    obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+    bdir = BUILD + ("_asan" if asan else "")
+    obj = os.path.join(bdir, os.path.basename(src) + ".o")
     if not _newer([src] + headers, obj):
         return obj
     common = ["-O3", "-fPIC", "-std=c++17", f"-I{CSRC}", "-Wno-unused-result"]
     if src.endswith(".hip"):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-x", "hip", "-c", src, "-o", obj, "-munsafe-fp-atomics"] + common
+        if asan:   # host half only: each -fsanitize right after -Xarch_host
+            cmd += [f for flag in ASAN_HOST for f in ("-Xarch_host", flag)]
     else:
         py_inc = sysconfig.get_paths()["include"]
         cmd = [HIPCC, "-c", src, "-o", obj, f"-I{pybind11.get_include()}", f"-I{py_inc}",
                "-D__HIP_PLATFORM_AMD__", "-fvisibility=hidden"] + common
+        if asan:
+            cmd += ASAN_HOST + ["-DCAN_MODULE_NAME=_C_asan"]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -56,16 +88,18 @@ def _compile(src: str, headers, verbose=False) -> str:
     return obj
 
 
-def build(jobs: int = 8, verbose: bool = False) -> str:
-    os.makedirs(BUILD, exist_ok=True)
+def build(jobs: int = 8, verbose: bool = False, asan: bool = False) -> str:
+    os.makedirs(BUILD + ("_asan" if asan else ""), exist_ok=True)
     headers = glob.glob(os.path.join(CSRC, "*.h"))
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, headers, verbose), srcs))
-    out = ext_path()
+        objs = list(ex.map(lambda s: _compile(s, headers, verbose, asan), srcs))
+    out = ext_path(asan)
     if _newer(objs, out):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs + [
             f"-L{ROCM}/lib", "-lamdhip64", "-lrccl", "-Wl,--no-undefined"]
+        if asan:
+            cmd += ["-fsanitize=address", "-shared-libasan"]
         py_lib = sysconfig.get_config_var("LIBDIR")
         if verbose:
             print(" ".join(cmd), flush=True)
@@ -84,5 +118,6 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 1))
     ap.add_argument("-v", action="store_true")
+    ap.add_argument("--asan", action="store_true", help="host-AddressSanitizer variant _C_asan")
     a = ap.parse_args()
-    print(build(a.j, a.v))
+    print(build(a.j, a.v, a.asan))

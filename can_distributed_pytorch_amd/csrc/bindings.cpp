@@ -26,7 +26,11 @@ static void check(int rc, const char* what) {
 
 #define P(x) reinterpret_cast<void*>(x)
 
-PYBIND11_MODULE(_C, m) {
+#ifndef CAN_MODULE_NAME
+#define CAN_MODULE_NAME _C   // _C_asan: the host-AddressSanitizer build (build_native.py --asan)
+#endif
+
+PYBIND11_MODULE(CAN_MODULE_NAME, m) {
   m.doc() = "gfx950 native kernels and runtime for can_distributed_pytorch_amd";
   register_rccl(m);
 

@@ -44,7 +44,10 @@ struct ConvArgs {
   int N, H, W, Cin, Cout, ksize, dil, M;
 };
 
-enum { EPI_BIAS_RELU = 0, EPI_MASK = 1, EPI_NONE = 2, EPI_BIAS = 3, EPI_SIGMOID = 4 };
+// EPI_POOLBWD (LDS-DMA kernels only): the GEMM output is the gradient of a 2x2/s2 max-pool output; the
+// epilogue scatters it straight into the pool INPUT gradient (a.mask = pool input, a.y = its gradient,
+// both [N][2H][2W][Cout]): first max of each window wins (ATen order), times the ReLU mask (max > 0).
+enum { EPI_BIAS_RELU = 0, EPI_MASK = 1, EPI_NONE = 2, EPI_BIAS = 3, EPI_SIGMOID = 4, EPI_POOLBWD = 5 };
 enum { LOAD_GENERIC = 0, LOAD_FIRST = 1 };
 
 __device__ __forceinline__ int perm_row(int rho) {
@@ -330,6 +333,40 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[j * 4 + r] = acc[j][i][r];
+    if constexpr (EPI == EPI_POOLBWD) {
+      // pooled pixel m = (n, ph, pw) -> window rows 2ph, 2ph+1, columns 2pw, 2pw+1 of the full map
+      const uint32_t q = fdiv((uint32_t)m, a.fdW);
+      const int pw = m - (int)q * a.W;
+      const uint32_t n = fdiv(q, a.fdH);
+      const int ph = (int)q - (int)n * a.H;
+      const size_t W2 = 2 * (size_t)a.W;
+      const size_t b0 = (((size_t)n * 2 * a.H + 2 * ph) * W2 + 2 * pw) * a.Cout + chb;
+      const size_t off[4] = {b0, b0 + a.Cout, b0 + W2 * a.Cout, b0 + W2 * a.Cout + a.Cout};
+      float x[4][16];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        unpack8h<DT>(*reinterpret_cast<const uint4*>(a.mask + off[w]), x[w]);
+        unpack8h<DT>(*reinterpret_cast<const uint4*>(a.mask + off[w] + 8), x[w] + 8);
+      }
+      float o[4][16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        int arg = 0;
+        float mv = x[0][c];
+#pragma unroll
+        for (int w = 1; w < 4; ++w)
+          if (x[w][c] > mv) { mv = x[w][c]; arg = w; }
+        const float gg = (mv > 0.f) ? v[c] : 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) o[w][c] = (w == arg) ? gg : 0.f;
+      }
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        *reinterpret_cast<uint4*>(a.y + off[w]) = pack8h<DT>(o[w]);
+        *reinterpret_cast<uint4*>(a.y + off[w] + 8) = pack8h<DT>(o[w] + 8);
+      }
+      continue;
+    }
     if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS) {
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
@@ -1002,7 +1039,8 @@ static int conv_igemm_impl(const void* x, const void* w, const float* bias, cons
     CAN_EPI_CASE(LOAD_FIRST, EPI_BIAS_RELU)
     return -5;
   }
-  if (auto_halo && Cin == 64 && ksize == 3 && dil == 1 && (Cout == 64 || Cout == 128) && epi != EPI_SIGMOID)
+  if (auto_halo && Cin == 64 && ksize == 3 && dil == 1 && (Cout == 64 || Cout == 128) && epi != EPI_SIGMOID &&
+      epi != EPI_POOLBWD)
     tile_cfg = 31;
   if (tile_cfg == 31) {
     // halo-tiled Cin = 64 kernel (explicit; see conv_halo64_kernel)
@@ -1036,6 +1074,7 @@ static int conv_igemm_impl(const void* x, const void* w, const float* bias, cons
       case EPI_NONE: return dispatch_glds<DT, EPI_NONE>(b, tile_cfg, s);
       case EPI_BIAS: return dispatch_glds<DT, EPI_BIAS>(b, tile_cfg, s);
       case EPI_SIGMOID: return dispatch_glds<DT, EPI_SIGMOID>(b, tile_cfg, s);
+      case EPI_POOLBWD: return dispatch_glds<DT, EPI_POOLBWD>(b, tile_cfg, s);
     }
     return -6;
   }

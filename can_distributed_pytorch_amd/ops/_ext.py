@@ -19,8 +19,9 @@ def load(build_if_missing: bool = False):
     global _mod, _err
     if _mod is not None:
         return _mod
+    name = "_C_asan" if os.environ.get("CANNET_ASAN", "0") == "1" else "_C"   # host-ASan build (build_native --asan)
     try:
-        _mod = importlib.import_module("can_distributed_pytorch_amd._C")
+        _mod = importlib.import_module("can_distributed_pytorch_amd." + name)
     except ImportError as e:  # pragma: no cover - depends on build state
         _err = e
         if build_if_missing or os.environ.get("CANNET_AUTOBUILD", "0") == "1":

@@ -22,7 +22,7 @@ import torch
 
 from . import _ext
 
-EPI_BIAS_RELU, EPI_MASK, EPI_NONE, EPI_BIAS = 0, 1, 2, 3
+EPI_BIAS_RELU, EPI_MASK, EPI_NONE, EPI_BIAS, EPI_SIGMOID, EPI_POOLBWD = 0, 1, 2, 3, 4, 5
 BF16 = torch.bfloat16
 ACT_DTYPES = {torch.bfloat16: 0, torch.float16: 1}   # -> kernel element-type code (csrc/common.h DT_*)
 
@@ -76,7 +76,10 @@ def _check_act(x: torch.Tensor, name: str, c: Optional[int] = None, dtype: Optio
 def conv_igemm(x: torch.Tensor, wpack: torch.Tensor, bias: Optional[torch.Tensor], *, ksize: int, dil: int = 1,
                epi: int = EPI_BIAS_RELU, mask: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
                first: bool = False, tile: int = 0) -> torch.Tensor:
-    """y[N,H,W,Co] = epi(conv(x[N,H,W,Ci], W) ...), stride 1, 'same' padding = dil*(ksize//2)."""
+    """y[N,H,W,Co] = epi(conv(x[N,H,W,Ci], W) ...), stride 1, 'same' padding = dil*(ksize//2).
+
+    epi=EPI_POOLBWD: the conv result is d(maxpool output); ``mask`` is the 2x2/s2 max-pool INPUT
+    [N,2H,2W,Co] and the result is written as d(pool input) * (pool max > 0) into [N,2H,2W,Co]."""
     C = _ext.require()
     if x.dim() != 4:
         raise ValueError("x must be [N,H,W,C]")
@@ -101,14 +104,17 @@ def conv_igemm(x: torch.Tensor, wpack: torch.Tensor, bias: Optional[torch.Tensor
     if epi in (EPI_BIAS_RELU, EPI_BIAS):
         if bias is None or bias.dtype != torch.float32 or bias.numel() != co or not bias.is_contiguous():
             raise ValueError("bias must be contiguous fp32 [Cout]")
-    if epi == EPI_MASK:
-        if mask is None or tuple(mask.shape) != (n, h, w, co):
-            raise ValueError("mask must be [N,H,W,Cout]")
+    oshape = (n, 2 * h, 2 * w, co) if epi == EPI_POOLBWD else (n, h, w, co)
+    if epi in (EPI_MASK, EPI_POOLBWD):
+        if mask is None or tuple(mask.shape) != oshape:
+            raise ValueError(f"mask must be {list(oshape)}")
         _check_act(mask, "mask", dtype=dt)
+        if epi == EPI_POOLBWD and (first or tile not in (0, 21, 22, 23, 25)):
+            raise ValueError("EPI_POOLBWD runs on the LDS-DMA kernels only")
     if out is None:
-        out = torch.empty(n, h, w, co, dtype=dt, device=x.device)
+        out = torch.empty(*oshape, dtype=dt, device=x.device)
     else:
-        if tuple(out.shape) != (n, h, w, co):
+        if tuple(out.shape) != oshape:
             raise ValueError("out has the wrong shape")
         _check_act(out, "out", dtype=dt)
     if n * h * w >= 2 ** 31 // max(ci, co):

@@ -29,6 +29,7 @@ Two ways in:
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional, Sequence
 
@@ -90,6 +91,7 @@ class CANNetExecutor:
         self._pack_desc_ptrs = None
         self.ws = None
         self.stream_override = None
+        self._side = None
 
     def grad_ready_order(self) -> List[int]:
         """Parameter indices in the order backward_features produces them."""
@@ -284,11 +286,15 @@ class CANNetExecutor:
         st = self._stream()
         ws = self.ws or self.workspace(*self._shape_from(sv))
         ready = on_grad_ready or (lambda idx: None)
+        side = self._side_stream()
+        hold = []          # operands of side-stream work, kept alive until the join below
 
         def wg(spec_or_w, dy, x, ksize, dil, first, wi, bi):
-            C.conv_wgrad(dy, x, grads[wi], grads[bi] if bi is not None else None, ksize=ksize, dil=dil, first=first,
-                         ws=ws, beta=beta, scale=scale, dscale=dscale)
-            ready([wi] + ([bi] if bi is not None else []))
+            def run():
+                C.conv_wgrad(dy, x, grads[wi], grads[bi] if bi is not None else None, ksize=ksize, dil=dil,
+                             first=first, ws=ws, beta=beta, scale=scale, dscale=dscale)
+                ready([wi] + ([bi] if bi is not None else []))
+            self._on_side(side, run, hold, dy, x)
 
         # ---- backend, reverse
         dy = d_b6
@@ -301,7 +307,7 @@ class CANNetExecutor:
             else:
                 dcat = C.conv_igemm(dy, dgr, None, ksize=3, dil=s.dil, epi=C.EPI_NONE)
         # ---- context module
-        dy = self._context_bwd(sv["ctx"], sv["fv"], dcat, grads, ws, beta, scale, ready, dscale)
+        dy = self._context_bwd(sv["ctx"], sv["fv"], dcat, grads, ws, beta, scale, ready, dscale, side, hold)
         # ---- frontend, reverse
         for s in reversed(self.front):
             x = sv["front_in"][s.idx]
@@ -311,17 +317,47 @@ class CANNetExecutor:
             _, dgr = self.packs[id(s.module.weight)]
             prev = self.front[s.idx - 1]
             if prev.pool_after:
-                dp = C.conv_igemm(dy, dgr, None, ksize=3, dil=1, epi=C.EPI_NONE)
+                # data gradient at the pooled resolution, scattered through the max-pool backward
+                # (+ ReLU mask of the pool input) in the conv epilogue: the pooled gradient never
+                # round-trips through memory
                 full = sv["pre_pool"][prev.idx]
-                dfull = torch.empty_like(full)
-                nn_, hh, ww, cc = full.shape
-                self.C.maxpool_bwd_relu(full.data_ptr(), dp.data_ptr(), dfull.data_ptr(), nn_, hh, ww, cc, self.dt,
-                                        st)
-                dy = dfull
+                if os.environ.get("CANNET_POOLBWD_FUSED", "1") != "0":
+                    dy = C.conv_igemm(dy, dgr, None, ksize=3, dil=1, epi=C.EPI_POOLBWD, mask=full)
+                else:
+                    dp = C.conv_igemm(dy, dgr, None, ksize=3, dil=1, epi=C.EPI_NONE)
+                    dy = torch.empty_like(full)
+                    nn_, hh, ww, cc = full.shape
+                    self.C.maxpool_bwd_relu(full.data_ptr(), dp.data_ptr(), dy.data_ptr(), nn_, hh, ww, cc, self.dt,
+                                            st)
             else:
                 dy = C.conv_igemm(dy, dgr, None, ksize=3, dil=1, epi=C.EPI_MASK, mask=x)
+        if side is not None:
+            torch.cuda.current_stream(d_b6.device).wait_stream(side)     # join: every gradient written
+        hold.clear()
 
-    def _context_bwd(self, ctx, fv, dcat, grads, ws, beta, scale, ready, dscale=None):
+    def _side_stream(self):
+        """Weight gradients run on a second stream, concurrently with the data-gradient chain (they only
+        need the layer's dY and input).  The memory-bound slab reductions / bias column sums and the
+        partial last waves of one chain fill the CUs the other leaves idle.  Fork/join through stream
+        waits, so the pattern is hipGraph-capturable; CANNET_WGRAD_STREAM=0 runs everything in order."""
+        if os.environ.get("CANNET_WGRAD_STREAM", "1") == "0" or self.stream_override is not None:
+            return None
+        dev = self.head.weight.device
+        if self._side is None or self._side.device != dev:
+            self._side = torch.cuda.Stream(dev)
+        return self._side
+
+    @staticmethod
+    def _on_side(side, fn, hold, *keep):
+        if side is None:
+            fn()
+            return
+        side.wait_stream(torch.cuda.current_stream(side.device))           # fork after the producers
+        with torch.cuda.stream(side):
+            fn()
+        hold.extend(keep)
+
+    def _context_bwd(self, ctx, fv, dcat, grads, ws, beta, scale, ready, dscale=None, side=None, hold=None):
         """Backward of the context module; returns d(F10 pre-activation) (ReLU mask of fv applied)."""
         st = self._stream()
         n, h, w, c = fv.shape
@@ -335,34 +371,44 @@ class CANNetExecutor:
             C.conv_igemm(dz[i], dgr, None, ksize=1, epi=C.EPI_NONE, out=dc[i])
         # the four conv{S}_2 weight gradients: one batched GEMM when their arena slots are adjacent
         dws = [grads[self.ctx2_index[sc]] for sc in CONTEXT_SCALES]
-        if C.wgrad_1x1_batched_ok(dz, ctx["cs"], dws):
-            C.conv_wgrad_1x1_batched(dz, ctx["cs"], dws, ws=ws, beta=beta, scale=scale, dscale=dscale)
-        else:
-            for i, sc in enumerate(CONTEXT_SCALES):
-                C.conv_wgrad(dz[i], ctx["cs"][i], dws[i], None, ksize=1, ws=ws, beta=beta, scale=scale, dscale=dscale)
-        ready([self.ctx2_index[sc] for sc in CONTEXT_SCALES])
+
+        def ctx2_wgrad():
+            if C.wgrad_1x1_batched_ok(dz, ctx["cs"], dws):
+                C.conv_wgrad_1x1_batched(dz, ctx["cs"], dws, ws=ws, beta=beta, scale=scale, dscale=dscale)
+            else:
+                for i, sc in enumerate(CONTEXT_SCALES):
+                    C.conv_wgrad(dz[i], ctx["cs"][i], dws[i], None, ksize=1, ws=ws, beta=beta, scale=scale,
+                                 dscale=dscale)
+            ready([self.ctx2_index[sc] for sc in CONTEXT_SCALES])
+        hold = [] if hold is None else hold
+        self._on_side(side, ctx2_wgrad, hold, dz)
         rowacc = ctx["rowacc"]
         dA = torch.empty(n, 50, c, dtype=torch.float32, device=fv.device)
         self.C.ctx_reduce(1, 0, sdir.data_ptr(), dc.data_ptr(), rowacc.data_ptr(), dA.data_ptr(), n, h, w, c, self.dt,
                           st)
         dave = torch.empty_like(dA)
         ave = ctx["ave"]
+
+        def ctx1_wgrad():
+            for sc in CONTEXT_SCALES:
+                o, k = CELL_OFF[sc], sc * sc
+                gA = dA[:, o:o + k].reshape(-1, c)
+                g = grads[self.ctx1_index[sc]].view(c, c)
+                gw = gA.t() @ ave[:, o:o + k].reshape(-1, c)
+                if scale != 1.0:
+                    gw = gw * scale
+                if dscale is not None:
+                    gw = gw * dscale
+                if beta:
+                    g.add_(gw)
+                else:
+                    g.copy_(gw)
+            ready([self.ctx1_index[sc] for sc in CONTEXT_SCALES])
+        self._on_side(side, ctx1_wgrad, hold, dA)
         for sc in CONTEXT_SCALES:
             o, k = CELL_OFF[sc], sc * sc
             w1 = self.ctx1[sc].weight.detach().view(c, c)
-            gA = dA[:, o:o + k].reshape(-1, c)
-            g = grads[self.ctx1_index[sc]].view(c, c)
-            gw = gA.t() @ ave[:, o:o + k].reshape(-1, c)
-            if scale != 1.0:
-                gw = gw * scale
-            if dscale is not None:
-                gw = gw * dscale
-            if beta:
-                g.add_(gw)
-            else:
-                g.copy_(gw)
             torch.matmul(dA[:, o:o + k], w1, out=dave[:, o:o + k])
-        ready([self.ctx1_index[sc] for sc in CONTEXT_SCALES])
         dfv = torch.empty(n, h, w, c, dtype=self.act, device=fv.device)
         self.C.ctx_bwd_final(dcat.data_ptr(), dc.data_ptr(), dave.data_ptr(), fv.data_ptr(), dfv.data_ptr(), n, h, w,
                              c, self.dt, st)

@@ -205,3 +205,24 @@ def test_conv_wgrad_v2_half_tiles(n, h, w, ci, co, dil, cfg, bias):
     _close(dw, gw, 1e-2)
     if bias:
         _close(db, gb, 1e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("n,h,w,ci,co", [(2, 12, 20, 128, 64), (1, 9, 13, 256, 128), (2, 6, 8, 512, 256)])
+def test_conv_dgrad_pool_backward_fused(n, h, w, ci, co, dtype):
+    """EPI_POOLBWD (dgrad + max-pool backward + ReLU mask in one epilogue) == EPI_NONE + maxpool_bwd_relu, bitwise."""
+    from can_distributed_pytorch_amd.ops import _ext
+    from can_distributed_pytorch_amd.ops import conv as C
+    torch.manual_seed(9)
+    wt = (torch.randn(ci, co, 3, 3, device="cuda") * 0.05).to(dtype).float()   # layer co -> ci (dgrad maps ci -> co)
+    dy = torch.randn(n, h, w, ci, device="cuda").to(dtype)
+    full = torch.relu(torch.randn(n, 2 * h, 2 * w, co, device="cuda")).to(dtype)
+    full[:, ::3, ::2] = 0                                          # ties and all-zero windows
+    pack = C.pack_weight_dgrad(wt, dtype)
+    fused = C.conv_igemm(dy, pack, None, ksize=3, epi=C.EPI_POOLBWD, mask=full)
+    dp = C.conv_igemm(dy, pack, None, ksize=3, epi=C.EPI_NONE)
+    ref = torch.empty_like(full)
+    _ext.require().maxpool_bwd_relu(full.data_ptr(), dp.data_ptr(), ref.data_ptr(), n, 2 * h, 2 * w, co,
+                                    C.dt_code(dtype), _ext.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(fused, ref)

@@ -67,7 +67,9 @@ def build_parser():
     p.add_argument("--dtype", choices=["bf16", "fp32", "fp16"], default="bf16")
     p.add_argument("--synthetic", type=str, default="", help="HxW: train/eval on synthetic crowds of this size")
     p.add_argument("--synthetic-n", type=int, default=64, help="synthetic train-set size (test set = n/4)")
-    p.add_argument("--graph", type=str2bool, default=None, help="hipGraph-capture the step (default: on for fixed-size synthetic data)")
+    p.add_argument("--graph", type=str2bool, default=False,
+                   help="hipGraph-capture the step (fixed-size inputs only; off by default: the eager step overlaps "
+                        "weight gradients on a side stream, which the ROCm graph serialises)")
     p.add_argument("--bucket-mb", type=float, default=25.0)
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--num-workers", type=int, default=4)
@@ -152,7 +154,7 @@ def main(args):
     # init-weight consistency (train.py:98-114 + DDP broadcast): one collective in the stepper
     from can_distributed_pytorch_amd.engine.trainer import build_trainer
     fixed = bool(args.synthetic)
-    graph = args.graph if args.graph is not None else (fixed and world == 1)
+    graph = bool(args.graph) and fixed
     if args.impl == "hip":
         stepper = build_trainer(impl="hip", dtype=args.dtype, device=device, world=world, lr=base_lr, graph=graph,
                                 model=model)
