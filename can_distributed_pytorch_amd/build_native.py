@@ -12,7 +12,8 @@ communicator, bucketed reducer) and the host side of every .hip translation
 unit (launch stubs, planning code) compiled with ``-fsanitize=address``; GPU
 code is NOT instrumented (``-Xarch_host``: device ASan is not available on this
 pool).  Load it with ``CANNET_ASAN=1`` under the ASan runtime, see
-``asan_env()`` / ``scripts/asan_check.sh``.
+``asan_env()`` / ``tests/test_asan_host.py`` (host-only paths: the ROCm ASan
+runtime's HSA interceptor aborts HIP allocations on this XNACK-off pool).
 """
 from __future__ import annotations
 
