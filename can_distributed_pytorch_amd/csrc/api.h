@@ -20,6 +20,13 @@ int can_conv_wgrad_1x1_batched(const void* dy, const void* x, float* ws, float* 
                                int nb, long long dy_bs, long long x_bs, long long dw_bs, int S, int mslice, float beta,
                                float scale, const float* dscale, int dt, void* stream);
 
+// conv1_2 with conv1_1's output recomputed from the NHWC4 image (never stored)
+int can_conv_f1(const void* x, const void* w, const float* bias, const void* img, const void* w1, const float* b1,
+                void* y, int N, int H, int W, int epi, int dt, void* stream);
+int can_conv_wgrad_f1(const void* dy, const void* img, const void* w1, const float* b1, float* ws, float* wsb,
+                      float* dw, float* db, int N, int H, int W, int S, float beta, float scale, const float* dscale,
+                      int dt, void* stream);
+
 // elementwise.hip
 int can_maxpool_fwd(const void* x, void* y, int N, int H, int W, int C, int dt, void* stream);
 int can_maxpool_bwd_relu(const void* x, const void* dy, void* dx, int N, int H, int W, int C, int dt, void* stream);

@@ -69,6 +69,20 @@ PYBIND11_MODULE(CAN_MODULE_NAME, m) {
           "conv_wgrad_1x1_batched");
   });
 
+  m.def("conv_f1", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t img, uintptr_t w1, uintptr_t b1, uintptr_t y,
+                      int N, int H, int W, int epi, int dt, uintptr_t stream) {
+    check(can_conv_f1(P(x), P(w), (const float*)bias, P(img), P(w1), (const float*)b1, P(y), N, H, W, epi, dt,
+                      P(stream)),
+          "conv_f1");
+  });
+  m.def("conv_wgrad_f1", [](uintptr_t dy, uintptr_t img, uintptr_t w1, uintptr_t b1, uintptr_t ws, uintptr_t wsb,
+                            uintptr_t dw, uintptr_t db, int N, int H, int W, int S, float beta, float scale,
+                            uintptr_t dscale, int dt, uintptr_t stream) {
+    check(can_conv_wgrad_f1(P(dy), P(img), P(w1), (const float*)b1, (float*)ws, (float*)wsb, (float*)dw, (float*)db,
+                            N, H, W, S, beta, scale, (const float*)dscale, dt, P(stream)),
+          "conv_wgrad_f1");
+  });
+
   // ---- elementwise
   m.def("maxpool_fwd", [](uintptr_t x, uintptr_t y, int N, int H, int W, int C, int dt, uintptr_t st) {
     check(can_maxpool_fwd(P(x), P(y), N, H, W, C, dt, P(st)), "maxpool_fwd");

@@ -134,6 +134,55 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// A-operand row order of the 16x16x32 MFMA convs: LDS / fragment row rho -> output channel, so
+// that lane q of the D layout (rows q*4+r of tile jt) owns channels q*16 + jt*4 + r, i.e. 16
+// CONSECUTIVE channels of one pixel per lane (two 16-B stores, no LDS round trip in epilogues).
+__device__ __forceinline__ int perm_row(int rho) {
+  // LDS weight row rho -> local output channel, so that lane q of the MFMA
+  // D layout (rows q*4+r of tile jt) owns channels q*16 + jt*4 + r.
+  const int rl = rho & 63;
+  return (rho & ~63) | (((rl >> 2) & 3) << 4) | ((rl >> 4) << 2) | (rl & 3);
+}
+
+// conv1_1 on MFMA for 16 pixels: lane (fr, fq) gets channels fq*16 + 4j + r (j, r < 4) of pixel fr
+// in acc[j][r] (same D layout as the halo kernels' accumulators: perm_row-packed A rows).  img4:
+// LDS image halo [rows][HCI] of 8-byte NHWC4 pixels; pixel fr's 3x3 window starts at pix0(fr).
+template <int DT>
+__device__ __forceinline__ void conv1_1_frag(const uint2* img4, int HCI, int pix0, const frag8_t (&w1f)[2][4],
+                                             f32x4 (&acc)[4], int fq) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int t0 = kk * 8 + fq * 2;                 // this lane's taps t0, t0 + 1 (k = tap*4 + c)
+    uint2 lo = make_uint2(0u, 0u), hi = make_uint2(0u, 0u);
+    if (t0 < 9) {
+      const int kh = (t0 * 11) >> 5, kw = t0 - kh * 3;
+      lo = img4[pix0 + kh * HCI + kw];
+    }
+    if (t0 + 1 < 9) {
+      const int kh = ((t0 + 1) * 11) >> 5, kw = t0 + 1 - kh * 3;
+      hi = img4[pix0 + kh * HCI + kw];
+    }
+    const frag8_t b = __builtin_bit_cast(frag8_t, make_uint4(lo.x, lo.y, hi.x, hi.y));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = mfma16<DT>(w1f[kk][j], b, acc[j]);
+  }
+}
+
+// A fragments of the packed first-layer weights (perm_row order), straight from global (8 KB, L2-hot)
+__device__ __forceinline__ void load_w1_frags(const bf16_t* w1, frag8_t (&w1f)[2][4], int fr, int fq) {
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      w1f[kk][j] = __builtin_bit_cast(frag8_t, *reinterpret_cast<const uint4*>(w1 + perm_row(j * 16 + fr) * 64 +
+                                                                                kk * 32 + fq * 8));
+}
+
+// TCOL = 64 (CO = 64 only): 4 waves, one per output row, 75 KB of LDS, so TWO
+// blocks share a CU and one block's halo fetch overlaps the other's MFMAs (the
+// 128-column block is alone on its CU: fetch, then compute, then store).
 // Bijective XCD-aware remap of a 1-D block id (MI355X: 8 XCDs, blocks dealt
 // round-robin).  Consecutive logical tiles land on the same XCD/L2.
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {

@@ -50,12 +50,6 @@ struct ConvArgs {
 enum { EPI_BIAS_RELU = 0, EPI_MASK = 1, EPI_NONE = 2, EPI_BIAS = 3, EPI_SIGMOID = 4, EPI_POOLBWD = 5 };
 enum { LOAD_GENERIC = 0, LOAD_FIRST = 1 };
 
-__device__ __forceinline__ int perm_row(int rho) {
-  // LDS weight row rho -> local output channel, so that lane q of the MFMA
-  // D layout (rows q*4+r of tile jt) owns channels q*16 + jt*4 + r.
-  const int rl = rho & 63;
-  return (rho & ~63) | (((rl >> 2) & 3) << 4) | ((rl >> 4) << 2) | (rl & 3);
-}
 
 __device__ __forceinline__ int swz(int row, int chunk) { return (chunk ^ (row & 7)); }
 
@@ -710,12 +704,16 @@ struct HaloConvArgs {
   bf16_t* y;
   const bf16_t* zero;
   int N, H, W, tiles_x, tiles_y;
+  // F1 recompute (conv_halo64_kernel<.., F1 = 1>): the network input NHWC4 image and the
+  // first layer (packed [64][64], k = tap*4 + c; fp32 bias).  conv1_1's output
+  // X2 = relu(conv1_1(img)) is never stored: EPI_BIAS_RELU rebuilds the X2 halo from
+  // the image (x is ignored), EPI_MASK rebuilds the ReLU mask (X2 > 0) of its outputs.
+  const bf16_t* img = nullptr;
+  const bf16_t* w1 = nullptr;
+  const float* b1 = nullptr;
 };
 
-// TCOL = 64 (CO = 64 only): 4 waves, one per output row, 75 KB of LDS, so TWO
-// blocks share a CU and one block's halo fetch overlaps the other's MFMAs (the
-// 128-column block is alone on its CU: fetch, then compute, then store).
-template <int DT, int CO, int EPI, int TCOL>
+template <int DT, int CO, int EPI, int TCOL, int F1 = 0>
 __global__ void __launch_bounds__((CO == 64 && TCOL == 64) ? 256 : 512, (TCOL == 64) ? 2 : 1)
 conv_halo64_kernel(HaloConvArgs a) {
   constexpr int TR = 4, HR = TR + 2, HC = TCOL + 2;
@@ -726,12 +724,16 @@ conv_halo64_kernel(HaloConvArgs a) {
   constexpr int WTAP = CO * 128;                      // one tap of weights: CO rows x 64 ci
   constexpr int GW = WTAP / 1024 / NW;                // weight DMA pieces per wave per tap
   constexpr int PW = CO / 64;                         // pixel fragments per wave / 4
+  // F1: image halo of the X2 halo (fwd: (HR+2) x (HC+2)) or of the output tile (mask: HR x HC)
+  constexpr int IHR = (EPI == EPI_MASK) ? HR : HR + 2, IHC = (EPI == EPI_MASK) ? HC : HC + 2;
   static_assert(GW >= 1, "weights split");
   static_assert(TCOL == 128 || (TCOL == 64 && CO == 64), "tile");
+  static_assert(!F1 || (CO == 64 && (EPI == EPI_BIAS_RELU || EPI == EPI_MASK)), "F1 recompute: conv1_2 fwd/dgrad");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* halo = smem;
   unsigned char* wring = smem + HALO_BYTES;
+  uint2* img4 = reinterpret_cast<uint2*>(wring + 3 * WTAP);   // F1 only: [IHR][IHC] image pixels
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
@@ -742,15 +744,42 @@ conv_halo64_kernel(HaloConvArgs a) {
   const int n = tile / (a.tiles_x * a.tiles_y);
   const int oh0 = ty * TR, ow0 = tx * TCOL;
 
-  // ---- halo DMA (once): piece i covers halo pixels 8i..8i+7
-  for (int i = wave; i < NHI; i += NW) {
-    const int hp = i * 8 + (lane >> 3);
-    const int hr = hp / HC, hc = hp - hr * HC;
-    const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
-    const void* src = a.zero;
-    if (hp < HPIX && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
-      src = a.x + ((size_t)(n * a.H + ih) * a.W + iw) * 64 + (((lane & 7) ^ (hc & 7)) * 8);
-    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(halo + i * 1024), 16, 0, 0);
+  // F1 forward: conv1_1's operands first, so the waits for them (vmcnt retires in issue order) never
+  // also wait for the weight-ring DMA issued below
+  frag8_t w1f[2][4];
+  float b1v[16];
+  if constexpr (F1 && EPI == EPI_BIAS_RELU) {
+    load_w1_frags(a.w1, w1f, lane & 15, lane >> 4);
+#pragma unroll
+    for (int c = 0; c < 16; c += 4) {
+      const float4 b4 = *reinterpret_cast<const float4*>(a.b1 + (lane >> 4) * 16 + c);
+      b1v[c] = b4.x; b1v[c + 1] = b4.y; b1v[c + 2] = b4.z; b1v[c + 3] = b4.w;
+    }
+  }
+  if constexpr (F1) {
+    // image pixels (8 B, NHWC4) of the region conv1_1 is recomputed on, zero outside the image
+    const int ir0 = (EPI == EPI_MASK) ? oh0 - 1 : oh0 - 2, ic0 = (EPI == EPI_MASK) ? ow0 - 1 : ow0 - 2;
+    const uint2* im = reinterpret_cast<const uint2*>(a.img);
+    for (int p = tid; p < IHR * IHC; p += NW * 64) {
+      const int rr = p / IHC, cc = p - rr * IHC;
+      const int ih = ir0 + rr, iw = ic0 + cc;
+      uint2 v = make_uint2(0u, 0u);
+      if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) v = im[(size_t)(n * a.H + ih) * a.W + iw];
+      img4[p] = v;
+    }
+    if constexpr (EPI == EPI_MASK) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read after the barriers
+  }
+  if constexpr (!F1 || EPI == EPI_MASK) {
+    // ---- halo DMA (once): piece i covers halo pixels 8i..8i+7
+    for (int i = wave; i < NHI; i += NW) {
+      const int hp = i * 8 + (lane >> 3);
+      const int hr = hp / HC, hc = hp - hr * HC;
+      const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
+      const void* src = a.zero;
+      if (hp < HPIX && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+        src = a.x + ((size_t)(n * a.H + ih) * a.W + iw) * 64 + (((lane & 7) ^ (hc & 7)) * 8);
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(halo + i * 1024), 16, 0, 0);
+    }
   }
   auto issue_w = [&](int t) {
     unsigned char* dst = wring + (t % 3) * WTAP;
@@ -764,6 +793,33 @@ conv_halo64_kernel(HaloConvArgs a) {
   };
   issue_w(0);
   issue_w(1);
+  const int fr = lane & 15, fq = lane >> 4;
+
+  if constexpr (F1 && EPI == EPI_BIAS_RELU) {
+    // X2 halo = relu(conv1_1(img) + b1) on MFMA, written in the DMA's layout (16-B channel chunk c of
+    // halo pixel (hr, hc) at chunk slot c ^ (hc & 7)); zero outside the image (conv1_2's padding)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // image halo in LDS
+    for (int g = wave; g * 16 < HPIX; g += NW) {
+      const int hp = g * 16 + fr;
+      const int hpc = hp < HPIX ? hp : HPIX - 1;
+      const int hr = hpc / HC, hc = hpc - hr * HC;
+      f32x4 x2[4];
+      conv1_1_frag<DT>(img4, IHC, hr * IHC + hc, w1f, x2, fq);
+      const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
+      const bool inside = ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[j * 4 + q] = inside ? fmaxf(x2[j][q] + b1v[j * 4 + q], 0.f) : 0.f;
+      if (hp < HPIX) {
+        uint4* dst = reinterpret_cast<uint4*>(halo + hp * 128);
+        dst[(2 * fq) ^ (hc & 7)] = pack8h<DT>(v);
+        dst[(2 * fq + 1) ^ (hc & 7)] = pack8h<DT>(v + 8);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // X2 halo stores done before the tap-0 barrier
+  }
 
   // wave -> (row, co half / column half)
   const int r = (NW == 4) ? wave : (wave >> 1);
@@ -778,7 +834,6 @@ conv_halo64_kernel(HaloConvArgs a) {
   // Per-lane LDS byte offsets, loop invariant: the halo swizzle is keyed by the
   // halo COLUMN (hc & 7 = (fr + kw) & 7 for every fragment and row), so each
   // fragment read is one ds_read_b128 at lane offset + compile-time immediate.
-  const int fr = lane & 15, fq = lane >> 4;
   int hoff[3][2], woff[2];
 #pragma unroll
   for (int kw = 0; kw < 3; ++kw)
@@ -819,16 +874,36 @@ conv_halo64_kernel(HaloConvArgs a) {
   if (oh >= a.H) return;
   const int chb = wc * 64 + fq * 16;
   float bias[16];
-  if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS) {
+  if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS || (F1 && EPI == EPI_MASK)) {
+    const float* bsrc = (F1 && EPI == EPI_MASK) ? a.b1 : a.bias;   // F1 mask: conv1_1's bias
 #pragma unroll
     for (int c = 0; c < 16; c += 4) {
-      const float4 b4 = *reinterpret_cast<const float4*>(a.bias + chb + c);
+      const float4 b4 = *reinterpret_cast<const float4*>(bsrc + chb + c);
       bias[c] = b4.x; bias[c + 1] = b4.y; bias[c + 2] = b4.z; bias[c + 3] = b4.w;
     }
   }
+  if constexpr (F1 && EPI == EPI_MASK) load_w1_frags(a.w1, w1f, fr, fq);   // all DMA has retired here
 #pragma unroll
   for (int i = 0; i < 4 * PW; ++i) {
     const int ow = ow0 + colbase + i * 16 + fr;
+    if constexpr (F1 && EPI == EPI_MASK) {
+      // the ReLU mask of conv1_2's input, recomputed: X2 = relu(conv1_1(img) + b1) > 0 at (oh, ow)
+      f32x4 x2[4];
+      conv1_1_frag<DT>(img4, IHC, r * IHC + colbase + i * 16 + fr, w1f, x2, fq);
+      if (ow >= a.W) continue;
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const bool pos = pos_bits(f2h<DT>(x2[j][q] + bias[j * 4 + q]));   // exactly the stored X2's sign
+          v[j * 4 + q] = pos ? acc[j][i][q] : 0.f;
+        }
+      const size_t off = ((size_t)(n * a.H + oh) * a.W + ow) * CO + chb;
+      *reinterpret_cast<uint4*>(a.y + off) = pack8h<DT>(v);
+      *reinterpret_cast<uint4*>(a.y + off + 8) = pack8h<DT>(v + 8);
+      continue;
+    }
     if (ow >= a.W) continue;
     float v[16];
 #pragma unroll
@@ -955,12 +1030,13 @@ __global__ void __launch_bounds__(512) conv_first_halo_kernel(HaloConvArgs a) {
   }
 }
 
-template <int DT, int CO, int EPI, int TCOL>
+template <int DT, int CO, int EPI, int TCOL, int F1 = 0>
 static int launch_halo64(const HaloConvArgs& a, hipStream_t s) {
   constexpr int HALO_BYTES = ((6 * (TCOL + 2) + 7) / 8) * 1024;
   constexpr int NW = (CO == 64 && TCOL == 64) ? 4 : 8;
-  const size_t lds = HALO_BYTES + 3 * (size_t)CO * 128;
-  auto kfn = conv_halo64_kernel<DT, CO, EPI, TCOL>;
+  constexpr int IMG_BYTES = !F1 ? 0 : (EPI == EPI_MASK) ? 6 * (TCOL + 2) * 8 : 8 * (TCOL + 4) * 8;
+  const size_t lds = HALO_BYTES + 3 * (size_t)CO * 128 + IMG_BYTES;
+  auto kfn = conv_halo64_kernel<DT, CO, EPI, TCOL, F1>;
   static bool attr = false;
   if (!attr) {
     CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -1087,7 +1163,28 @@ static int conv_igemm_impl(const void* x, const void* w, const float* bias, cons
   return -6;
 }
 
+// conv1_2 with conv1_1 recomputed (its output never stored): epi EPI_BIAS_RELU = forward from the image,
+// EPI_MASK = data gradient (x = dY of conv1_2) with the ReLU mask of conv1_1 recomputed.
+template <int DT>
+static int conv_f1_impl(const void* x, const void* w, const float* bias, const void* img, const void* w1,
+                        const float* b1, void* y, int N, int H, int W, int epi, hipStream_t s) {
+  HaloConvArgs h;
+  h.x = (const bf16_t*)x; h.w = (const bf16_t*)w; h.bias = bias; h.mask = nullptr; h.y = (bf16_t*)y;
+  h.zero = conv_zero_page();
+  if (!h.zero) return -10;
+  h.img = (const bf16_t*)img; h.w1 = (const bf16_t*)w1; h.b1 = b1;
+  h.N = N; h.H = H; h.W = W; h.tiles_x = (W + 63) / 64; h.tiles_y = (H + 3) / 4;
+  if (epi == EPI_BIAS_RELU) return launch_halo64<DT, 64, EPI_BIAS_RELU, 64, 1>(h, s);
+  if (epi == EPI_MASK) return launch_halo64<DT, 64, EPI_MASK, 64, 1>(h, s);
+  return -6;
+}
+
 }  // namespace can
+
+extern "C" int can_conv_f1(const void* x, const void* w, const float* bias, const void* img, const void* w1,
+                           const float* b1, void* y, int N, int H, int W, int epi, int dt, void* stream) {
+  CAN_DT_DISPATCH(dt, can::conv_f1_impl<DT>(x, w, bias, img, w1, b1, y, N, H, W, epi, (hipStream_t)stream));
+}
 
 // dt: element type of x / w / mask / y (DT_BF16 = 0, DT_F16 = 1)
 extern "C" int can_conv_igemm(const void* x, const void* w, const float* bias, const void* mask, void* y,

@@ -798,9 +798,14 @@ struct HaloArgs {
   float* wsb;
   int N, H, W, Cin, Cout, K, S;
   int tiles_y, tiles_x, ntiles, tiles_per_slice;
+  // F1 (wgrad_halo_kernel<.., F1 = 1>, conv1_2): x is the NHWC4 network input and the layer input
+  // X2 = relu(conv1_1(x) + b1) is recomputed per stage from a 6 x 68 image halo (3.3 KB instead of
+  // the 33 KB X2 halo), so conv1_1's output is never stored.
+  const bf16_t* w1 = nullptr;
+  const float* b1 = nullptr;
 };
 
-template <int DT, int CO, int TH>
+template <int DT, int CO, int TH, int F1 = 0>
 __global__ void __launch_bounds__(576, 1) wgrad_halo_kernel(HaloArgs a) {
   constexpr int TW = 64;
   constexpr int HW_ = TW + 2;                       // halo width
@@ -809,10 +814,12 @@ __global__ void __launch_bounds__(576, 1) wgrad_halo_kernel(HaloArgs a) {
   constexpr int RBD = CO * 2;                       // dY row bytes
   constexpr int DY_BYTES = NPIX * RBD;
   constexpr int X_BYTES = ((HH * HW_ * 128 + 1023) / 1024) * 1024;
-  constexpr int STAGE = DY_BYTES + X_BYTES;
+  constexpr int IMG_BYTES = F1 ? ((HH + 2) * (HW_ + 2) * 8 + 1023) / 1024 * 1024 : 0;   // F1: image halo
+  constexpr int STAGE = DY_BYTES + X_BYTES + IMG_BYTES;
   constexpr int NID = DY_BYTES / 1024;              // LDS-DMA instructions per stage
-  constexpr int NIX = X_BYTES / 1024;
+  constexpr int NIX = F1 ? IMG_BYTES / 1024 : X_BYTES / 1024;
   constexpr int NT = CO / 16;                       // co tiles of 16
+  static_assert(!F1 || CO == 64, "F1: conv1_2 (64 -> 64)");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -828,13 +835,15 @@ __global__ void __launch_bounds__(576, 1) wgrad_halo_kernel(HaloArgs a) {
   const int nstage = max(0, t_end - t_beg);
   const bool do_bias = (a.wsb != nullptr) && ci_t == 0 && wave == 4;
 
-  auto issue = [&](int st, int buf) {
+  // i_lo .. i_hi: the stage's DMA pieces to issue (dY pieces [0, NID), X / image pieces [NID, NID + NIX))
+  auto issue = [&](int st, int buf, int i_lo = 0, int i_hi = -1) {
+    if (i_hi < 0) i_hi = NID + NIX;
     const int t = t_beg + st;
     const int n = t / (a.tiles_y * a.tiles_x);
     const int rem = t - n * a.tiles_y * a.tiles_x;
     const int y0 = (rem / a.tiles_x) * TH, x0 = (rem % a.tiles_x) * TW;
     unsigned char* sbase = smem + buf * STAGE;
-    for (int i = wave; i < NID + NIX; i += 9) {
+    for (int i = i_lo + (wave + 9 - i_lo % 9) % 9; i < i_hi; i += 9) {
       const void* src = a.zero;
       unsigned char* dst;
       if (i < NID) {
@@ -844,6 +853,14 @@ __global__ void __launch_bounds__(576, 1) wgrad_halo_kernel(HaloArgs a) {
         const int yy = y0 + p / TW, xx = x0 + p % TW;
         if (yy < a.H && xx < a.W) src = a.dy + ((size_t)(n * a.H + yy) * a.W + xx) * a.Cout + co0 + lc16 * 8;
         dst = sbase + i * 1024;
+      } else if constexpr (F1) {
+        // image halo rows y0-2 .. y0+TH+1, columns x0-2 .. x0+65, 2 pixels (16 B) per lane: x0 - 2 and
+        // W are even, so both pixels of a pair are inside or both outside the image
+        const int q2 = ((i - NID) * 1024 + lane * 16) / 8;   // first pixel of the pair
+        const int yy = y0 - 2 + q2 / (HW_ + 2), xx = x0 - 2 + q2 % (HW_ + 2);
+        if (q2 < (HH + 2) * (HW_ + 2) && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W)
+          src = a.x + ((size_t)(n * a.H + yy) * a.W + xx) * 4;
+        dst = sbase + DY_BYTES + X_BYTES + (i - NID) * 1024;
       } else {
         const int byte = (i - NID) * 1024 + lane * 16;
         const int q = byte / 128;
@@ -854,6 +871,66 @@ __global__ void __launch_bounds__(576, 1) wgrad_halo_kernel(HaloArgs a) {
         dst = sbase + DY_BYTES + (i - NID) * 1024;
       }
       __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+  };
+  // F1: X2 = relu(conv1_1(img) + b1) of the stage's (HH x HW_) halo into the X image, in the layout the
+  // DMA would have produced (16-B channel chunk c of row q at slot c ^ k2(q)); zero outside the image
+  // conv1_1's packed weights (8 KB) and bias live in LDS behind the two stage buffers and are re-read
+  // there every stage: 9 waves on 4 SIMDs leave no room to keep 48 more registers live across the
+  // stage loop, and a global (vmcnt-counted) reload inside the loop would wait for the next stage's
+  // DMA too (vmcnt retires in issue order)
+  unsigned char* w1s = smem + 2 * STAGE;
+  if constexpr (F1) {
+    for (int i = tid; i < 64 * 64 / 8; i += 576)
+      reinterpret_cast<uint4*>(w1s)[i] = reinterpret_cast<const uint4*>(a.w1)[i];
+    if (tid < 64) reinterpret_cast<float*>(w1s + 64 * 64 * 2)[tid] = a.b1[tid];
+  }
+  auto build_x2 = [&](int st, int buf) {
+    const int t = t_beg + st;
+    const int n = t / (a.tiles_y * a.tiles_x);
+    const int rem = t - n * a.tiles_y * a.tiles_x;
+    const int y0 = (rem / a.tiles_x) * TH, x0 = (rem % a.tiles_x) * TW;
+    unsigned char* Xb = smem + buf * STAGE + DY_BYTES;
+    const uint2* img4 = reinterpret_cast<const uint2*>(Xb + X_BYTES);
+    const int fr = lane & 15, fq = lane >> 4;
+    const bf16_t* w1l = reinterpret_cast<const bf16_t*>(w1s);
+    const float* b1s = reinterpret_cast<const float*>(w1s + 64 * 64 * 2);
+    for (int gidx = wave; gidx * 16 < HH * HW_; gidx += 9) {
+      const int qp = gidx * 16 + fr;
+      const int qc = qp < HH * HW_ ? qp : HH * HW_ - 1;
+      const int hr = qc / HW_, hc = qc - hr * HW_;
+      // im2col fragments of the pixel (taps t0, t0+1 of each K half), then one 16-channel tile at a
+      // time (few live registers: the 9-wave kernel sits at the 170-VGPR occupancy limit)
+      frag8_t bim[2];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int t0 = kk * 8 + fq * 2;
+        uint2 lo = make_uint2(0u, 0u), hi = make_uint2(0u, 0u);
+        const int pix0 = hr * (HW_ + 2) + hc;
+        if (t0 < 9) lo = img4[pix0 + ((t0 * 11) >> 5) * (HW_ + 2) + t0 - ((t0 * 11) >> 5) * 3];
+        if (t0 + 1 < 9) hi = img4[pix0 + (((t0 + 1) * 11) >> 5) * (HW_ + 2) + t0 + 1 - (((t0 + 1) * 11) >> 5) * 3];
+        bim[kk] = __builtin_bit_cast(frag8_t, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      }
+      const int yy = y0 - 1 + hr, xx = x0 - 1 + hc;
+      const bool inside = yy >= 0 && yy < a.H && xx >= 0 && xx < a.W && qp < HH * HW_;
+      const int k2 = ((((qp >> 1) & 1) | (((qp >> 3) & 1) << 1)) << 1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        f32x4 x2 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const frag8_t wf = __builtin_bit_cast(
+              frag8_t, *reinterpret_cast<const uint4*>(w1l + perm_row(j * 16 + fr) * 64 + kk * 32 + fq * 8));
+          x2 = mfma16<DT>(wf, bim[kk], x2);
+        }
+        // channels fq*16 + 4j .. +3 of pixel qp: 8 bytes = half (j & 1) of 16-B chunk 2*fq + (j >> 1)
+        float v[4];
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) v[q4] = inside ? fmaxf(x2[q4] + b1s[fq * 16 + j * 4 + q4], 0.f) : 0.f;
+        if (qp < HH * HW_)
+          *reinterpret_cast<uint2*>(Xb + qp * 128 + (((2 * fq + (j >> 1)) ^ k2) * 16) + (j & 1) * 8) =
+              make_uint2(pack2<DT>(v[0], v[1]), pack2<DT>(v[2], v[3]));
+      }
     }
   };
 
@@ -882,10 +959,27 @@ __global__ void __launch_bounds__(576, 1) wgrad_halo_kernel(HaloArgs a) {
   using RBdy = std::integral_constant<int, RBD>;
   using RBx = std::integral_constant<int, 128>;
 
-  if (nstage > 0) issue(0, 0);
+  if constexpr (F1) {
+    // software pipeline: the image halo runs two stages ahead of dY and X2(st + 1) is built in the same
+    // barrier phase as stage st's MFMAs, so one wave's build overlaps the other waves' matrix work.
+    // Buffer b = s & 1 holds dY(s), X2(s) and image(s) or image(s + 2) (image(s) is dead once X2(s) is
+    // built, one phase before image(s + 2) is issued into it)
+    if (nstage > 0) issue(0, 0);
+    if (nstage > 1) issue(1, 1, NID, NID + NIX);
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (nstage > 0) build_x2(0, 0);
+  } else {
+    if (nstage > 0) issue(0, 0);
+  }
   for (int st = 0; st < nstage; ++st) {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (st + 1 < nstage) issue(st + 1, (st + 1) & 1);
+    if constexpr (F1) {
+      if (st + 1 < nstage) issue(st + 1, (st + 1) & 1, 0, NID);
+      if (st + 2 < nstage) issue(st + 2, st & 1, NID, NID + NIX);
+      if (st + 1 < nstage) build_x2(st + 1, (st + 1) & 1);
+    } else {
+      if (st + 1 < nstage) issue(st + 1, (st + 1) & 1);
+    }
     const unsigned char* Db = smem + (st & 1) * STAGE;
     const unsigned char* Xb = Db + DY_BYTES;
 #pragma unroll
@@ -929,13 +1023,14 @@ __global__ void __launch_bounds__(576, 1) wgrad_halo_kernel(HaloArgs a) {
   }
 }
 
-template <int DT, int CO, int TH>
+template <int DT, int CO, int TH, int F1 = 0>
 static int launch_halo(HaloArgs& a, hipStream_t s) {
   constexpr int TW = 64;
   constexpr int DY_BYTES = TH * TW * CO * 2;
   constexpr int X_BYTES = (((TH + 2) * (TW + 2) * 128 + 1023) / 1024) * 1024;
-  const size_t lds = 2 * (size_t)(DY_BYTES + X_BYTES);
-  auto kfn = wgrad_halo_kernel<DT, CO, TH>;
+  constexpr int IMG_BYTES = F1 ? ((TH + 4) * (TW + 4) * 8 + 1023) / 1024 * 1024 : 0;
+  const size_t lds = 2 * (size_t)(DY_BYTES + X_BYTES + IMG_BYTES) + (F1 ? 64 * 64 * 2 + 64 * 4 : 0);
+  auto kfn = wgrad_halo_kernel<DT, CO, TH, F1>;
   static bool attr = false;
   if (!attr) {
     CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -1293,4 +1388,32 @@ extern "C" int can_conv_wgrad_1x1_batched(const void* dy, const void* x, float* 
                                           void* stream) {
   CAN_DT_DISPATCH(dt, conv_wgrad_1x1_batched_impl<DT>(dy, x, ws, dw, M, W, Cin, Cout, nb, dy_bs, x_bs, dw_bs, S,
                                                       mslice, beta, scale, dscale, (hipStream_t)stream));
+}
+
+// conv1_2 weight gradient with its input X2 = relu(conv1_1(img) + b1) recomputed from the NHWC4 image
+// (conv1_1's output is never stored).  dY [N,H,W,64], img [N,H,W,4], w1 packed [64][64], b1 fp32 [64].
+template <int DT>
+static int conv_wgrad_f1_impl(const void* dy, const void* img, const void* w1, const float* b1, float* ws, float* wsb,
+                              float* dw, float* db, int N, int H, int W, int S, float beta, float scale,
+                              const float* dscale, hipStream_t s) {
+  using namespace can;
+  if (W % 2 || S < 1) return -3;
+  HaloArgs h;
+  h.dy = (const bf16_t*)dy; h.x = (const bf16_t*)img; h.zero = zero_page(); h.ws = ws;
+  h.wsb = (db != nullptr) ? wsb : nullptr;
+  if (!h.zero) return -7;
+  h.N = N; h.H = H; h.W = W; h.Cin = 64; h.Cout = 64; h.K = 576; h.S = S;
+  h.tiles_y = (H + 1) / 2; h.tiles_x = (W + 63) / 64; h.ntiles = N * h.tiles_y * h.tiles_x;
+  h.tiles_per_slice = (h.ntiles + S - 1) / S;
+  h.w1 = (const bf16_t*)w1; h.b1 = b1;
+  int rc = launch_halo<DT, 64, 2, 1>(h, s);
+  if (rc) return rc;
+  return launch_reduce2(ws, h.wsb, dw, db, S, S, 576, 64, 64, 9, 0, beta, scale, dscale, s);
+}
+
+extern "C" int can_conv_wgrad_f1(const void* dy, const void* img, const void* w1, const float* b1, float* ws,
+                                 float* wsb, float* dw, float* db, int N, int H, int W, int S, float beta, float scale,
+                                 const float* dscale, int dt, void* stream) {
+  CAN_DT_DISPATCH(dt, conv_wgrad_f1_impl<DT>(dy, img, w1, b1, ws, wsb, dw, db, N, H, W, S, beta, scale, dscale,
+                                             (hipStream_t)stream));
 }

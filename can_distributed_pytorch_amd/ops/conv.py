@@ -228,3 +228,78 @@ def conv_wgrad_1x1_batched(dy: torch.Tensor, x: torch.Tensor, dws, *, ws: "Wgrad
                              m * co, m * ci, co * ci, s, mslice, float(beta), float(scale),
                              dscale.data_ptr() if dscale is not None else 0, dt_code(dy.dtype),
                              _ext.stream_ptr(x.device))
+
+
+# ----------------------------------------------------------------------------------------------
+# conv1_2 with conv1_1 recomputed.  X2 = relu(conv1_1(img) + b1) (64 channels at full resolution,
+# 805 MB per 8 x 768 x 1024 batch) is never stored: the conv1_2 forward rebuilds its X2 halo from
+# the NHWC4 image, the data gradient rebuilds conv1_1's ReLU mask, and the weight gradient rebuilds
+# its X2 tiles per stage.  ~4.5 GB less HBM traffic per training step at batch 8.
+# ----------------------------------------------------------------------------------------------
+F1_WGRAD_SLICES = 512
+
+
+def _check_f1(img: torch.Tensor, w1pack: torch.Tensor, b1: torch.Tensor, dt):
+    if img.dim() != 4 or img.shape[-1] != 4:
+        raise ValueError("img must be the NHWC4 network input [N,H,W,4]")
+    _check_act(img, "img", dtype=dt)
+    if tuple(w1pack.shape) != (64, 64) or w1pack.dtype != dt or not w1pack.is_contiguous():
+        raise ValueError("w1pack must be the packed first-layer weight [64,64] of the activation dtype")
+    if b1.dtype != torch.float32 or b1.numel() != 64 or not b1.is_contiguous():
+        raise ValueError("b1 must be contiguous fp32 [64]")
+    if img.shape[2] % 2:
+        raise ValueError("W must be even")
+
+
+def conv_f1(x: Optional[torch.Tensor], wpack: torch.Tensor, bias: Optional[torch.Tensor], img: torch.Tensor,
+            w1pack: torch.Tensor, b1: torch.Tensor, *, epi: int) -> torch.Tensor:
+    """epi=EPI_BIAS_RELU: conv1_2 forward, relu(conv(X2, wpack) + bias) with X2 recomputed from img (x unused).
+    epi=EPI_MASK: conv1_2 data gradient, conv(x = dY, flipped wpack) * (X2 > 0) with X2 recomputed."""
+    C = _ext.require()
+    dt = img.dtype
+    _check_f1(img, w1pack, b1, dt)
+    n, h, w, _ = img.shape
+    if tuple(wpack.shape) != (64, 576) or wpack.dtype != dt or not wpack.is_contiguous():
+        raise ValueError("wpack must be a packed [64, 9*64] conv1_2 weight")
+    if epi == EPI_BIAS_RELU:
+        if bias is None or bias.dtype != torch.float32 or bias.numel() != 64:
+            raise ValueError("bias must be fp32 [64]")
+        xp = 0
+    elif epi == EPI_MASK:
+        if x is None or tuple(x.shape) != (n, h, w, 64):
+            raise ValueError("x (dY) must be [N,H,W,64]")
+        _check_act(x, "x", dtype=dt)
+        xp = x.data_ptr()
+    else:
+        raise ValueError("conv_f1 supports EPI_BIAS_RELU and EPI_MASK")
+    out = torch.empty(n, h, w, 64, dtype=dt, device=img.device)
+    C.conv_f1(xp, wpack.data_ptr(), bias.data_ptr() if bias is not None else 0, img.data_ptr(), w1pack.data_ptr(),
+              b1.data_ptr(), out.data_ptr(), n, h, w, epi, dt_code(dt), _ext.stream_ptr(img.device))
+    return out
+
+
+def conv_wgrad_f1_need(m: int) -> int:
+    return F1_WGRAD_SLICES * 576 * 64 + max(F1_WGRAD_SLICES, 512) * 64
+
+
+def conv_wgrad_f1(dy: torch.Tensor, img: torch.Tensor, w1pack: torch.Tensor, b1: torch.Tensor, dw: torch.Tensor,
+                  db: Optional[torch.Tensor], *, ws: WgradWorkspace, beta: float = 0.0, scale: float = 1.0,
+                  dscale: Optional[torch.Tensor] = None) -> None:
+    """conv1_2 weight / bias gradient with its input X2 = relu(conv1_1(img) + b1) recomputed."""
+    C = _ext.require()
+    dt = dy.dtype
+    _check_act(dy, "dy", 64)
+    _check_f1(img, w1pack, b1, dt)
+    n, h, w, _ = img.shape
+    if tuple(dy.shape) != (n, h, w, 64):
+        raise ValueError("dy must be [N,H,W,64]")
+    if tuple(dw.shape) != (64, 64, 3, 3) or dw.dtype != torch.float32 or not dw.is_contiguous():
+        raise ValueError("dw must be contiguous fp32 [64,64,3,3]")
+    if db is not None and (db.dtype != torch.float32 or db.numel() != 64):
+        raise ValueError("db must be fp32 [64]")
+    s = F1_WGRAD_SLICES
+    buf = ws.reserve(conv_wgrad_f1_need(n * h * w))
+    C.conv_wgrad_f1(dy.data_ptr(), img.data_ptr(), w1pack.data_ptr(), b1.data_ptr(), buf.data_ptr(),
+                    buf.data_ptr() + 4 * s * 576 * 64, dw.data_ptr(), db.data_ptr() if db is not None else 0, n, h, w,
+                    s, float(beta), float(scale), dscale.data_ptr() if dscale is not None else 0, dt_code(dt),
+                    _ext.stream_ptr(img.device))

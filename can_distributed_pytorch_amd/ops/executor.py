@@ -180,6 +180,7 @@ class CANNetExecutor:
             need = max(need, self.ws.plan(n * hh * ww, s.cin, s.cout, 3, False)[3])
         need = max(need, self.ws.plan(n * hh * ww, 512, 512, 1, False)[3])
         need = max(need, C.wgrad_1x1_batched_plan(n * hh * ww, 4, 512, 512)[2])
+        need = max(need, C.conv_wgrad_f1_need(n * h * w))
         self.ws.reserve(need)
         return self.ws
 
@@ -212,16 +213,37 @@ class CANNetExecutor:
         self.C.img_to_nhwc4(img.data_ptr(), x4.data_ptr(), n, h, w, self.dt, self._stream())
         return x4
 
+    def _f1_fused(self) -> bool:
+        """Opt-in (CANNET_F1_FUSED=1): conv1_1's output is recomputed inside conv1_2's kernels instead
+        of being stored.  Measured at 768x1024 batch 8 (profiles/r1_native/f1_recompute.txt): forward
+        -0.27 ms and data gradient even, but the weight gradient's per-stage recompute of the 4 x 66
+        halo (2x the 2 x 64 output rows it feeds) costs +0.38 ms, so the stored path stays the default."""
+        f0, f1 = self.front[0], self.front[1]
+        return (os.environ.get("CANNET_F1_FUSED", "0") == "1" and f0.first and f0.cout == 64 and f1.cin == 64 and
+                f1.cout == 64 and f1.ksize == 3 and f1.dil == 1)
+
+    def _f1_args(self):
+        f0 = self.front[0]
+        return self.packs[id(f0.module.weight)][0], f0.module.bias.detach()
+
     def forward_features(self, img, save: bool):
         """Runs everything up to the last backend ReLU. Returns (b6 [N,h,w,64], saved dict)."""
         self.refresh_packs()
         sv = {} if save else None
         x = self._img(img)
-        acts = []   # conv inputs of the frontend
+        acts = []   # conv inputs of the frontend (conv1_2's is the image too when conv1_1 is recomputed)
         pre_pool = {}
+        f1 = self._f1_fused()
         for s in self.front:
             acts.append(x)
-            y = self._conv(s, x)
+            if f1 and s.idx == 0:
+                continue                     # conv1_1 runs inside conv1_2's kernels
+            if f1 and s.idx == 1:
+                w1, b1 = self._f1_args()
+                fwd, _ = self.packs[id(s.module.weight)]
+                y = C.conv_f1(None, fwd, s.module.bias.detach(), acts[0], w1, b1, epi=C.EPI_BIAS_RELU)
+            else:
+                y = self._conv(s, x)
             if s.pool_after:
                 pre_pool[s.idx] = y
                 x = self._maxpool(y)
@@ -235,7 +257,7 @@ class CANNetExecutor:
             back_in.append(x)
             x = self._conv(s, x)
         if save:
-            sv.update(front_in=acts, pre_pool=pre_pool, fv=fv, ctx=ctx_saved, back_in=back_in, b6=x)
+            sv.update(front_in=acts, pre_pool=pre_pool, fv=fv, ctx=ctx_saved, back_in=back_in, b6=x, f1=f1)
         return x, sv
 
     def _context_fwd(self, fv, save):
@@ -311,6 +333,19 @@ class CANNetExecutor:
         # ---- frontend, reverse
         for s in reversed(self.front):
             x = sv["front_in"][s.idx]
+            if sv.get("f1") and s.idx == 1:
+                # conv1_2 with conv1_1's output recomputed from the image (x) in both kernels
+                w1, b1 = self._f1_args()
+                _, dgr = self.packs[id(s.module.weight)]
+                dy2 = dy
+
+                def run_f1(dy2=dy2, x=x, s=s):
+                    C.conv_wgrad_f1(dy2, x, w1, b1, grads[s.w_index], grads[s.b_index], ws=ws, beta=beta,
+                                    scale=scale, dscale=dscale)
+                    ready([s.w_index, s.b_index])
+                self._on_side(side, run_f1, hold, dy2, x)
+                dy = C.conv_f1(dy, dgr, None, x, w1, b1, epi=C.EPI_MASK)
+                continue
             wg(s, dy, x, 3, 1, s.first, s.w_index, s.b_index)
             if s.idx == 0:
                 break

@@ -226,3 +226,37 @@ def test_conv_dgrad_pool_backward_fused(n, h, w, ci, co, dtype):
                                     C.dt_code(dtype), _ext.stream_ptr())
     torch.cuda.synchronize()
     assert torch.equal(fused, ref)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("n,h,w", [(2, 40, 136), (1, 301, 900)])
+def test_conv1_2_with_conv1_1_recomputed_is_bitwise_stored_path(n, h, w, dtype):
+    """conv1_2 fwd / dgrad / wgrad with conv1_1's output recomputed from the image == the stored-X2 path, bitwise
+    (same MFMA K order for conv1_1, same rounding)."""
+    from can_distributed_pytorch_amd.ops import conv as C
+    torch.manual_seed(10)
+    img = torch.randn(n, 3, h, w, device="cuda")
+    x4 = C.to_nhwc4(img, dtype)
+    w1 = (torch.randn(64, 3, 3, 3, device="cuda") * 0.2).to(dtype).float()
+    b1 = torch.randn(64, device="cuda") * 0.1
+    w2 = (torch.randn(64, 64, 3, 3, device="cuda") * 0.05).to(dtype).float()
+    b2 = torch.randn(64, device="cuda") * 0.1
+    w1p = C.pack_weight_first(w1, dtype)
+    x2 = C.conv_igemm(x4, w1p, b1, ksize=3, first=True)
+    y_ref = C.conv_igemm(x2, C.pack_weight_fwd(w2, dtype), b2, ksize=3)
+    y = C.conv_f1(None, C.pack_weight_fwd(w2, dtype), b2, x4, w1p, b1, epi=C.EPI_BIAS_RELU)
+    assert torch.equal(y, y_ref)
+    dy = torch.randn(n, h, w, 64, device="cuda").to(dtype)
+    dx_ref = C.conv_igemm(dy, C.pack_weight_dgrad(w2, dtype), None, ksize=3, epi=C.EPI_MASK, mask=x2)
+    dx = C.conv_f1(dy, C.pack_weight_dgrad(w2, dtype), None, x4, w1p, b1, epi=C.EPI_MASK)
+    assert torch.equal(dx, dx_ref)
+    ws = C.WgradWorkspace("cuda")
+    dw_ref, db_ref = torch.empty(64, 64, 3, 3, device="cuda"), torch.empty(64, device="cuda")
+    dw, db = torch.empty_like(dw_ref), torch.empty_like(db_ref)
+    C.conv_wgrad(dy, x2, dw_ref, db_ref, ksize=3, ws=ws)
+    C.conv_wgrad_f1(dy, x4, w1p, b1, dw, db, ws=ws)
+    if n * h * w >= 262144:          # both on the halo kernel with the same slicing: bitwise
+        assert torch.equal(dw, dw_ref) and torch.equal(db, db_ref)
+    else:
+        _close(dw, dw_ref, 1e-3)
+        _close(db, db_ref, 1e-3)

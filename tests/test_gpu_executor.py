@@ -169,3 +169,27 @@ def test_batched_packs_match_reference_packing():
         w = conv.weight.detach()
         assert torch.equal(fwd, C.pack_weight_fwd(w))
         assert torch.equal(dgr, C.pack_weight_dgrad(w))
+
+
+def test_native_stepper_f1_recompute_matches_stored(monkeypatch):
+    """conv1_1 recomputed inside conv1_2's kernels (CANNET_F1_FUSED=1) trains like the stored path."""
+    from can_distributed_pytorch_amd.engine.native import NativeStepper
+    _, nat_a = _models(6)
+    nat_b = copy.deepcopy(nat_a)
+    init = [(n, p.detach().clone()) for n, p in nat_a.named_parameters()]
+    x = torch.randn(2, 3, 64, 128, device="cuda")
+    gt = torch.rand(2, 1, 8, 16, device="cuda")
+    a = NativeStepper("cuda", lr=1e-7, graph=False, model=nat_a)
+    b = NativeStepper("cuda", lr=1e-7, graph=False, model=nat_b)
+    la, lb = [], []
+    for _ in range(3):
+        monkeypatch.setenv("CANNET_F1_FUSED", "0")
+        la.append(float(a.step(x, gt)))
+        monkeypatch.setenv("CANNET_F1_FUSED", "1")
+        lb.append(float(b.step(x, gt)))
+    torch.cuda.synchronize()
+    assert b.ex._f1_fused()
+    for u, v in zip(la, lb):
+        assert abs(u - v) <= 1e-3 * abs(u), (la, lb)
+    for (name, p0), pa, pb in zip(init, nat_a.parameters(), nat_b.parameters()):
+        assert _rel(pb - p0, pa - p0) < 2e-2, name    # the updates, not the weights
