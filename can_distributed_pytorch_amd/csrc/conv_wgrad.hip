@@ -1073,6 +1073,30 @@ namespace can {
 // block dispatch for S ~ 7 and planes of millions of elements).  Each group
 // sums slices sl = g, g+SG, ... in order with 4 accumulators; groups combine in
 // LDS in a fixed order: deterministic.  The last Cout/16 blocks reduce the bias parts.
+// bias: block = 16 channels x 16 part groups (group g sums parts g, g+16, ...), fixed order
+__device__ __forceinline__ void reduce_bias_block(const float* __restrict__ wsb, float* __restrict__ db, int Sb,
+                                                  int Cout, float beta, float scale, int bb, float (&bpart)[16][16]) {
+  const int c = bb * 16 + (threadIdx.x & 15), g = threadIdx.x >> 4;
+  float t0 = 0.f, t1 = 0.f;
+  if (c < Cout) {
+    int sl = g;
+    for (; sl + 16 < Sb; sl += 32) {
+      t0 += wsb[(size_t)sl * Cout + c];
+      t1 += wsb[(size_t)(sl + 16) * Cout + c];
+    }
+    if (sl < Sb) t0 += wsb[(size_t)sl * Cout + c];
+  }
+  bpart[g][threadIdx.x & 15] = t0 + t1;
+  __syncthreads();
+  if (g == 0 && c < Cout) {
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v += bpart[q][threadIdx.x & 15];
+    v *= scale;
+    db[c] = (beta != 0.f) ? db[c] * beta + v : v;
+  }
+}
+
 template <int SG>
 __global__ void __launch_bounds__(256) wgrad_reduce2_kernel(const float* __restrict__ ws, const float* __restrict__ wsb,
                                                             float* __restrict__ dw, float* __restrict__ db, int S,
@@ -1088,26 +1112,7 @@ __global__ void __launch_bounds__(256) wgrad_reduce2_kernel(const float* __restr
   const int nbias = (db != nullptr) ? (Cout + 15) / 16 : 0;
   const int nmain = gridDim.x - nbias;
   if ((int)blockIdx.x >= nmain) {
-    // bias: block = 16 channels x 16 part groups (group g sums parts g, g+16, ...)
-    const int c = ((int)blockIdx.x - nmain) * 16 + (threadIdx.x & 15), g = threadIdx.x >> 4;
-    float t0 = 0.f, t1 = 0.f;
-    if (c < Cout) {
-      int sl = g;
-      for (; sl + 16 < Sb; sl += 32) {
-        t0 += wsb[(size_t)sl * Cout + c];
-        t1 += wsb[(size_t)(sl + 16) * Cout + c];
-      }
-      if (sl < Sb) t0 += wsb[(size_t)sl * Cout + c];
-    }
-    bpart[g][threadIdx.x & 15] = t0 + t1;
-    __syncthreads();
-    if (g == 0 && c < Cout) {
-      float v = 0.f;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) v += bpart[q][threadIdx.x & 15];
-      v *= scale;
-      db[c] = (beta != 0.f) ? db[c] * beta + v : v;
-    }
+    reduce_bias_block(wsb, db, Sb, Cout, beta, scale, (int)blockIdx.x - nmain, bpart);
     return;
   }
   const int cin_t = first ? 3 : Cin;
@@ -1150,12 +1155,78 @@ __global__ void __launch_bounds__(256) wgrad_reduce2_kernel(const float* __restr
   }
 }
 
+// Tiled form for 3x3 layers with few slabs (S <= 16): block = 64 output channels x RCI input channels x 9 taps.
+// Slab rows (tap, ci) are read as 256-B runs of 64 co, summed over the slabs in order, transposed through LDS
+// and written as 64 contiguous runs of RCI*9 floats of dW[co][ci][tap] (the grid-stride form writes dW with a
+// Cin*9-float stride between neighbouring lanes: one 4-B store per 64-B line).
+constexpr int RCI = 8;
+__global__ void __launch_bounds__(256) wgrad_reduce_tiled_kernel(const float* __restrict__ ws,
+                                                                 const float* __restrict__ wsb,
+                                                                 float* __restrict__ dw, float* __restrict__ db,
+                                                                 int S, int Sb, int Cout, int Cin, float beta,
+                                                                 float scale, const float* __restrict__ dscale) {
+  constexpr int ROWS = 9 * RCI, LD = 68;          // (tap, ci) rows of 64 co, padded to 68 floats
+  __shared__ __attribute__((aligned(16))) float tile[ROWS * LD];
+  __shared__ float bpart[16][16];
+  if (dscale != nullptr) scale *= dscale[0];
+  const int nco = Cout >> 6, nci = Cin / RCI;
+  const int nmain = nco * nci;
+  if ((int)blockIdx.x >= nmain) {
+    reduce_bias_block(wsb, db, Sb, Cout, beta, scale, (int)blockIdx.x - nmain, bpart);
+    return;
+  }
+  const int co0 = ((int)blockIdx.x % nco) * 64, ci0 = ((int)blockIdx.x / nco) * RCI;
+  const size_t plane = (size_t)9 * Cin * Cout;
+  const int c4 = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  for (int row = rg; row < ROWS; row += 16) {
+    const int t = row / RCI, ci = row - t * RCI;
+    const float* src = ws + ((size_t)(t * Cin + ci0 + ci) * Cout + co0 + c4 * 4);
+    // same summation order as wgrad_reduce2_kernel<1> (4 accumulators over slabs sl, sl+1, sl+2, sl+3)
+    float4 acc[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    int sl = 0;
+    for (; sl + 3 < S; sl += 4) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(src + (size_t)(sl + u) * plane);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc[u].x += v[u].x; acc[u].y += v[u].y; acc[u].z += v[u].z; acc[u].w += v[u].w;
+      }
+    }
+    for (; sl < S; ++sl) {
+      const float4 v = *reinterpret_cast<const float4*>(src + (size_t)sl * plane);
+      acc[0].x += v.x; acc[0].y += v.y; acc[0].z += v.z; acc[0].w += v.w;
+    }
+    *reinterpret_cast<float4*>(tile + row * LD + c4 * 4) =
+        make_float4(((acc[0].x + acc[1].x) + (acc[2].x + acc[3].x)) * scale,
+                    ((acc[0].y + acc[1].y) + (acc[2].y + acc[3].y)) * scale,
+                    ((acc[0].z + acc[1].z) + (acc[2].z + acc[3].z)) * scale,
+                    ((acc[0].w + acc[1].w) + (acc[2].w + acc[3].w)) * scale);
+  }
+  __syncthreads();
+  // dW[co][ci0 .. ci0 + RCI)[0 .. 9) is RCI*9 contiguous floats per co
+  for (int e = threadIdx.x; e < 64 * ROWS; e += 256) {
+    const int co = e / ROWS, rem = e - co * ROWS;
+    const int ci = rem / 9, t = rem - ci * 9;
+    const float v = tile[(t * RCI + ci) * LD + co];
+    float* o = dw + ((size_t)(co0 + co) * Cin + ci0) * 9 + rem;
+    *o = (beta != 0.f) ? (*o * beta + v) : v;
+  }
+}
+
 static int launch_reduce2(const float* ws, const float* wsb, float* dw, float* db, int S, int Sb, int K, int Cout,
                           int Cin, int taps, int first, float beta, float scale, const float* dscale, hipStream_t s) {
   const size_t plane = (size_t)K * Cout;
   const int nbias = (db != nullptr) ? (Cout + 15) / 16 : 0;
   auto grid = [&](int epb) { return (int)std::min<size_t>((plane + epb - 1) / epb, 4096) + nbias; };
-  if (S <= 16)
+  const bool tiled_off = getenv("CANNET_REDUCE_GRIDSTRIDE") != nullptr;   // A/B switch, read per launch
+  if (!tiled_off && !first && taps == 9 && S <= 16 && Cout % 64 == 0 && Cin % RCI == 0 &&
+      (Cout / 64) * (Cin / RCI) >= 256) {
+    hipLaunchKernelGGL(wgrad_reduce_tiled_kernel, dim3((Cout / 64) * (Cin / RCI) + nbias), dim3(256), 0, s, ws, wsb,
+                       dw, db, S, Sb, Cout, Cin, beta, scale, dscale);
+  } else if (S <= 16)
     hipLaunchKernelGGL(wgrad_reduce2_kernel<1>, dim3(grid(256)), dim3(256), 0, s, ws, wsb, dw, db, S, Sb, K, Cout,
                        Cin, taps, first, beta, scale, dscale);
   else if (S <= 128)

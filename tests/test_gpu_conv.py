@@ -207,6 +207,33 @@ def test_conv_wgrad_v2_half_tiles(n, h, w, ci, co, dil, cfg, bias):
         _close(db, gb, 1e-2)
 
 
+@pytest.mark.parametrize("n,h,w,ci,co,dil,beta", [(2, 8, 64, 512, 256, 2, 0.0), (1, 6, 128, 1024, 512, 1, 1.0),
+                                                    (2, 5, 64, 256, 512, 2, 0.5)])
+def test_wgrad_tiled_reduction_matches_grid_stride(n, h, w, ci, co, dil, beta, monkeypatch):
+    """The LDS-transposing slab reduction (coalesced dW writes) == the grid-stride one, bitwise, beta included."""
+    from can_distributed_pytorch_amd.ops import conv as C
+    torch.manual_seed(11)
+    x = torch.randn(n, h, w, ci, device="cuda").to(torch.bfloat16)
+    dy = torch.randn(n, h, w, co, device="cuda").to(torch.bfloat16)
+    dw0 = torch.randn(co, ci, 3, 3, device="cuda")
+    db0 = torch.randn(co, device="cuda")
+    out = []
+    for env in ("1", None):
+        if env:
+            monkeypatch.setenv("CANNET_REDUCE_GRIDSTRIDE", env)
+        else:
+            monkeypatch.delenv("CANNET_REDUCE_GRIDSTRIDE", raising=False)
+        dw, db = dw0.clone(), db0.clone()
+        C.conv_wgrad(dy, x, dw, db, ksize=3, dil=dil, beta=beta, scale=0.25)
+        torch.cuda.synchronize()
+        out.append((dw, db))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    wr = torch.zeros(co, ci, 3, 3, device="cuda", requires_grad=True)
+    y = F.conv2d(x.float().permute(0, 3, 1, 2), wr, None, padding=dil, dilation=dil)
+    (gw,) = torch.autograd.grad(y, (wr,), dy.float().permute(0, 3, 1, 2))
+    _close(out[1][0], beta * dw0 + 0.25 * gw, 1e-2)
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("n,h,w,ci,co", [(2, 12, 20, 128, 64), (1, 9, 13, 256, 128), (2, 6, 8, 512, 256)])
 def test_conv_dgrad_pool_backward_fused(n, h, w, ci, co, dtype):
