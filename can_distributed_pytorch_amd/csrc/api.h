@@ -20,6 +20,11 @@ int can_conv_wgrad_1x1_batched(const void* dy, const void* x, float* ws, float* 
                                int nb, long long dy_bs, long long x_bs, long long dw_bs, int S, int mslice, float beta,
                                float scale, const float* dscale, int dt, void* stream);
 
+// conv + bias + ReLU with the 2x2/s2 max-pool fused into the epilogue (y full resolution, yp pooled)
+int can_conv_pool_fwd(const void* x, const void* w, const float* bias, void* y, void* yp, int N, int H, int W,
+                      int Cin, int Cout, int ksize, int dil, int tile_cfg, int dt, void* stream);
+int can_conv_pool_tp(int Cin, int Cout, int ksize, int tile_cfg);
+
 // conv1_2 with conv1_1's output recomputed from the NHWC4 image (never stored)
 int can_conv_f1(const void* x, const void* w, const float* bias, const void* img, const void* w1, const float* b1,
                 void* y, int N, int H, int W, int epi, int dt, void* stream);

@@ -69,6 +69,14 @@ PYBIND11_MODULE(CAN_MODULE_NAME, m) {
           "conv_wgrad_1x1_batched");
   });
 
+  m.def("conv_pool_fwd", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, uintptr_t yp, int N, int H, int W,
+                            int Cin, int Cout, int ksize, int dil, int tile_cfg, int dt, uintptr_t stream) {
+    check(can_conv_pool_fwd(P(x), P(w), (const float*)bias, P(y), P(yp), N, H, W, Cin, Cout, ksize, dil, tile_cfg,
+                            dt, P(stream)),
+          "conv_pool_fwd");
+  });
+  m.def("conv_pool_tp", &can_conv_pool_tp);
+
   m.def("conv_f1", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t img, uintptr_t w1, uintptr_t b1, uintptr_t y,
                       int N, int H, int W, int epi, int dt, uintptr_t stream) {
     check(can_conv_f1(P(x), P(w), (const float*)bias, P(img), P(w1), (const float*)b1, P(y), N, H, W, epi, dt,

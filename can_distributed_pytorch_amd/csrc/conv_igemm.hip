@@ -47,7 +47,13 @@ struct ConvArgs {
 // EPI_POOLBWD (LDS-DMA kernels only): the GEMM output is the gradient of a 2x2/s2 max-pool output; the
 // epilogue scatters it straight into the pool INPUT gradient (a.mask = pool input, a.y = its gradient,
 // both [N][2H][2W][Cout]): first max of each window wins (ATen order), times the ReLU mask (max > 0).
-enum { EPI_BIAS_RELU = 0, EPI_MASK = 1, EPI_NONE = 2, EPI_BIAS = 3, EPI_SIGMOID = 4, EPI_POOLBWD = 5 };
+// EPI_POOLFWD (LDS-DMA v2 kernel only, H even, W % (TP/2) == 0): bias + ReLU like EPI_BIAS_RELU, and
+// the 2x2/s2 max-pool of the result is written to a.yp [N][H/2][W/2][Cout] in the same epilogue.  A pixel
+// tile is then 2 image rows x TP/2 columns with the rows interleaved inside each 16-pixel MFMA fragment
+// (fragment f, row fr: column f*8 + fr/2, row fr&1), so every pool window sits in 4 adjacent lanes and is
+// reduced with two DPP quad permutes (the pooled map is never re-read from HBM by a separate pass).
+enum { EPI_BIAS_RELU = 0, EPI_MASK = 1, EPI_NONE = 2, EPI_BIAS = 3, EPI_SIGMOID = 4, EPI_POOLBWD = 5,
+       EPI_POOLFWD = 6 };
 enum { LOAD_GENERIC = 0, LOAD_FIRST = 1 };
 
 
@@ -199,7 +205,7 @@ conv_igemm_kernel(ConvArgs a) {
   // ---- epilogue: lane owns channels [chb, chb+16) of one pixel per tile i
   const int chb = ct * TC + wc * 64 + fq * 16;
   float bias[16];
-  if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS) {
+  if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS || EPI == EPI_POOLFWD) {
 #pragma unroll
     for (int c = 0; c < 16; c += 4) {
       const float4 b4 = *reinterpret_cast<const float4*>(a.bias + chb + c);
@@ -215,11 +221,11 @@ conv_igemm_kernel(ConvArgs a) {
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[j * 4 + r] = acc[j][i][r];
-    if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS) {
+    if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS || EPI == EPI_POOLFWD) {
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         v[c] += bias[c];
-        if (EPI == EPI_BIAS_RELU) v[c] = fmaxf(v[c], 0.f);
+        if (EPI != EPI_BIAS) v[c] = fmaxf(v[c], 0.f);
       }
     }
     if (EPI == EPI_SIGMOID) {
@@ -301,7 +307,21 @@ struct ConvArgs2 {
   const bf16_t* zero;
   int H, W, Cin, Cout, ksize, dil, M;
   FastDiv fdW, fdH;
+  bf16_t* yp = nullptr;   // EPI_POOLFWD: pooled output [N][H/2][W/2][Cout]
 };
+
+// pixel m of row r of pixel tile pt; EPI_POOLFWD tiles are 2 rows x TP/2 columns, rows interleaved per
+// 16-pixel fragment (see EPI_POOLFWD), the other epilogues take TP consecutive pixels
+template <int TP, int EPI>
+__device__ __forceinline__ int tile_pix(const ConvArgs2& a, int pt, int r) {
+  if constexpr (EPI == EPI_POOLFWD) {
+    const int ncb = a.W / (TP / 2);
+    const int rp = pt / ncb, cb = pt - rp * ncb;    // rp = n * H/2 + pooled row
+    return (2 * rp + (r & 1)) * a.W + cb * (TP / 2) + (r >> 4) * 8 + ((r & 15) >> 1);
+  } else {
+    return pt * TP + r;
+  }
+}
 
 // Shared epilogue of the LDS-DMA kernels: lane (fr, fq) of wave (wc, wp) owns
 // 16 consecutive output channels of one pixel per 16x16 pixel fragment.
@@ -311,7 +331,7 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
   constexpr int TC = 64 * WC, TP = 64 * PW * WP;
   const int chb = ct * TC + wc * 64 + fq * 16;
   float bias[16];
-  if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS) {
+  if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS || EPI == EPI_POOLFWD) {
 #pragma unroll
     for (int c = 0; c < 16; c += 4) {
       const float4 b4 = *reinterpret_cast<const float4*>(a.bias + chb + c);
@@ -320,7 +340,7 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
   }
 #pragma unroll
   for (int i = 0; i < 4 * PW; ++i) {
-    const int m = pt * TP + wp * 64 * PW + i * 16 + fr;
+    const int m = tile_pix<TP, EPI>(a, pt, wp * 64 * PW + i * 16 + fr);
     if (m >= a.M) continue;
     float v[16];
 #pragma unroll
@@ -361,11 +381,11 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
       }
       continue;
     }
-    if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS) {
+    if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS || EPI == EPI_POOLFWD) {
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         v[c] += bias[c];
-        if (EPI == EPI_BIAS_RELU) v[c] = fmaxf(v[c], 0.f);
+        if (EPI != EPI_BIAS) v[c] = fmaxf(v[c], 0.f);
       }
     }
     if (EPI == EPI_SIGMOID) {
@@ -384,10 +404,35 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
         v[c] = pos ? v[c] : 0.f;
       }
     }
-    *reinterpret_cast<uint4*>(a.y + off) =
+    const uint4 o0 =
         make_uint4(pack2<DT>(v[0], v[1]), pack2<DT>(v[2], v[3]), pack2<DT>(v[4], v[5]), pack2<DT>(v[6], v[7]));
-    *reinterpret_cast<uint4*>(a.y + off + 8) =
+    const uint4 o1 =
         make_uint4(pack2<DT>(v[8], v[9]), pack2<DT>(v[10], v[11]), pack2<DT>(v[12], v[13]), pack2<DT>(v[14], v[15]));
+    *reinterpret_cast<uint4*>(a.y + off) = o0;
+    *reinterpret_cast<uint4*>(a.y + off + 8) = o1;
+    if constexpr (EPI == EPI_POOLFWD) {
+      // lanes 4q .. 4q+3 hold the window (2 columns x 2 rows) of one pooled pixel: max of the stored
+      // (rounded) values over quad_perm [1,0,3,2] then [2,3,0,1]
+      float r[16];
+      unpack8h<DT>(o0, r);
+      unpack8h<DT>(o1, r + 8);
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        float t = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(r[c]), 0xB1, 0xF, 0xF, false));
+        r[c] = fmaxf(r[c], t);
+        t = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(r[c]), 0x4E, 0xF, 0xF, false));
+        r[c] = fmaxf(r[c], t);
+      }
+      if ((fr & 3) == 0) {
+        const int ncb = a.W / (TP / 2);
+        const int rp = pt / ncb, cb = pt - rp * ncb;
+        const int pr = wp * 64 * PW + i * 16 + fr;
+        const int pc = cb * (TP / 4) + (pr >> 4) * 4 + ((pr & 15) >> 2);
+        bf16_t* yp = a.yp + ((size_t)rp * (a.W >> 1) + pc) * a.Cout + chb;
+        *reinterpret_cast<uint4*>(yp) = pack8h<DT>(r);
+        *reinterpret_cast<uint4*>(yp + 8) = pack8h<DT>(r + 8);
+      }
+    }
   }
 }
 
@@ -538,7 +583,7 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
 #pragma unroll
   for (int j = 0; j < GB; ++j) {
     const int r = (wave + NW * j) * 8 + (lane >> 3);
-    const int m = pt * TP + r;
+    const int m = tile_pix<TP, EPI>(a, pt, r);
     unsigned msk = 0;
     if (m < a.M) {
       const uint32_t q = fdiv((uint32_t)m, a.fdW);
@@ -910,11 +955,11 @@ conv_halo64_kernel(HaloConvArgs a) {
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int q = 0; q < 4; ++q) v[j * 4 + q] = acc[j][i][q];
-    if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS) {
+    if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS || EPI == EPI_POOLFWD) {
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         v[c] += bias[c];
-        if (EPI == EPI_BIAS_RELU) v[c] = fmaxf(v[c], 0.f);
+        if (EPI != EPI_BIAS) v[c] = fmaxf(v[c], 0.f);
       }
     }
     const size_t off = ((size_t)(n * a.H + oh) * a.W + ow) * CO + chb;
@@ -1061,17 +1106,27 @@ static int launch_glds(const ConvArgs2& a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// default LDS-DMA tile config: v2 (pipelined); 128 x 512 tiles measured faster for K <= 1152
+static int glds_default_cfg(int Cin, int Cout, int ksize) {
+  const int ktot = ksize * ksize * Cin;
+  return (Cout % 256 == 0) ? 21 : (Cout % 128 == 0) ? (ktot <= 1152 ? 25 : 22) : 23;
+}
+static int glds_cfg_tp(int cfg) {   // pixels per tile of a v2 config
+  return (cfg == 21 || cfg == 22) ? 256 : (cfg == 23 || cfg == 25) ? 512 : 0;
+}
+
 template <int DT, int EPI>
 static int dispatch_glds(const ConvArgs2& a, int tile_cfg, hipStream_t s) {
   int cfg = tile_cfg;
-  if (cfg == 0) {   // v2 (pipelined) by default; 128 x 512 tiles measured faster for K <= 1152
-    const int ktot = a.ksize * a.ksize * a.Cin;
-    cfg = (a.Cout % 256 == 0) ? 21 : (a.Cout % 128 == 0) ? (ktot <= 1152 ? 25 : 22) : 23;
+  if (cfg == 0) cfg = glds_default_cfg(a.Cin, a.Cout, a.ksize);
+  if constexpr (EPI == EPI_POOLFWD) {
+    const int tp = glds_cfg_tp(cfg);
+    if (tp == 0 || (a.H & 1) || a.W % (tp / 2) || a.yp == nullptr) return -12;
   }
   switch (cfg) {
-    case 11: if (a.Cout % 256) return -8; return launch_glds<DT, 4, 2, 2, EPI>(a, s);
-    case 12: if (a.Cout % 128) return -8; return launch_glds<DT, 2, 4, 1, EPI>(a, s);
-    case 13: return launch_glds<DT, 1, 8, 1, EPI>(a, s);
+    case 11: if (a.Cout % 256 || EPI == EPI_POOLFWD) return -8; return launch_glds<DT, 4, 2, 2, EPI>(a, s);
+    case 12: if (a.Cout % 128 || EPI == EPI_POOLFWD) return -8; return launch_glds<DT, 2, 4, 1, EPI>(a, s);
+    case 13: if (EPI == EPI_POOLFWD) return -8; return launch_glds<DT, 1, 8, 1, EPI>(a, s);
     case 21: if (a.Cout % 256) return -8; return launch_glds2<DT, 4, 2, 2, EPI>(a, s);
     case 22: if (a.Cout % 128) return -8; return launch_glds2<DT, 2, 4, 1, EPI>(a, s);
     case 23: return launch_glds2<DT, 1, 8, 1, EPI>(a, s);
@@ -1163,6 +1218,21 @@ static int conv_igemm_impl(const void* x, const void* w, const float* bias, cons
   return -6;
 }
 
+// 3x3 / 1x1 conv + bias + ReLU with the 2x2/s2 max-pool fused into the epilogue: y = full-resolution
+// output (kept for the backward pass), yp = pooled output.  LDS-DMA v2 kernels only.
+template <int DT>
+static int conv_pool_fwd_impl(const void* x, const void* w, const float* bias, void* y, void* yp, int N, int H,
+                              int W, int Cin, int Cout, int ksize, int dil, int tile_cfg, hipStream_t s) {
+  if (Cout % 64 || Cin % 64 || H < 2 || W < 2) return -3;
+  ConvArgs2 b;
+  b.x = (const bf16_t*)x; b.w = (const bf16_t*)w; b.bias = bias; b.mask = nullptr; b.y = (bf16_t*)y;
+  b.yp = (bf16_t*)yp; b.zero = conv_zero_page();
+  if (!b.zero) return -10;
+  b.H = H; b.W = W; b.Cin = Cin; b.Cout = Cout; b.ksize = ksize; b.dil = dil; b.M = N * H * W;
+  b.fdW = make_fastdiv((uint32_t)W); b.fdH = make_fastdiv((uint32_t)H);
+  return dispatch_glds<DT, EPI_POOLFWD>(b, tile_cfg, s);
+}
+
 // conv1_2 with conv1_1 recomputed (its output never stored): epi EPI_BIAS_RELU = forward from the image,
 // EPI_MASK = data gradient (x = dY of conv1_2) with the ReLU mask of conv1_1 recomputed.
 template <int DT>
@@ -1192,4 +1262,16 @@ extern "C" int can_conv_igemm(const void* x, const void* w, const float* bias, c
                               int epi, int first, int tile_cfg, int dt, void* stream) {
   CAN_DT_DISPATCH(dt, can::conv_igemm_impl<DT>(x, w, bias, mask, y, N, H, W, Cin, Cout, ksize, dil, epi, first,
                                               tile_cfg, stream));
+}
+
+extern "C" int can_conv_pool_fwd(const void* x, const void* w, const float* bias, void* y, void* yp, int N, int H,
+                                 int W, int Cin, int Cout, int ksize, int dil, int tile_cfg, int dt, void* stream) {
+  CAN_DT_DISPATCH(dt, can::conv_pool_fwd_impl<DT>(x, w, bias, y, yp, N, H, W, Cin, Cout, ksize, dil, tile_cfg,
+                                              (hipStream_t)stream));
+}
+
+// pixels per tile of the kernel conv_pool_fwd runs for this layer (tile_cfg 0 = default): the fused pool
+// needs H even and W % (tp / 2) == 0
+extern "C" int can_conv_pool_tp(int Cin, int Cout, int ksize, int tile_cfg) {
+  return can::glds_cfg_tp(tile_cfg ? tile_cfg : can::glds_default_cfg(Cin, Cout, ksize));
 }

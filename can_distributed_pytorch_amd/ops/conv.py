@@ -251,6 +251,46 @@ def _check_f1(img: torch.Tensor, w1pack: torch.Tensor, b1: torch.Tensor, dt):
         raise ValueError("W must be even")
 
 
+def conv_pool_fwd_ok(x: torch.Tensor, cout: int, ksize: int, tile: int = 0) -> bool:
+    """Whether conv_pool_fwd covers this layer: H even and W a multiple of half the kernel's pixel tile."""
+    n, h, w, ci = x.shape
+    if ci % 64 or cout % 64 or h % 2 or h < 2 or w < 2:
+        return False
+    tp = _ext.require().conv_pool_tp(ci, cout, ksize, tile)
+    return tp > 0 and w % (tp // 2) == 0
+
+
+def conv_pool_fwd(x: torch.Tensor, wpack: torch.Tensor, bias: torch.Tensor, *, ksize: int, dil: int = 1,
+                  out: Optional[torch.Tensor] = None, pooled: Optional[torch.Tensor] = None, tile: int = 0):
+    """relu(conv(x, W) + b) -> (y [N,H,W,Co], maxpool2x2(y) [N,H/2,W/2,Co]) in one kernel: the pool runs in the
+    conv epilogue on the rounded outputs, so both tensors equal conv_igemm(EPI_BIAS_RELU) + maxpool_fwd bitwise."""
+    C = _ext.require()
+    _check_act(x, "x")
+    n, h, w, ci = x.shape
+    co, k = wpack.shape
+    dt = x.dtype
+    if wpack.dtype != dt or not wpack.is_contiguous() or k != ksize * ksize * ci:
+        raise ValueError("wpack must be the contiguous packed forward weight of this layer")
+    if bias is None or bias.dtype != torch.float32 or bias.numel() != co or not bias.is_contiguous():
+        raise ValueError("bias must be contiguous fp32 [Cout]")
+    if not conv_pool_fwd_ok(x, co, ksize, tile):
+        raise ValueError(f"fused pool needs H even and W a multiple of the tile half-width ({list(x.shape)})")
+    if n * h * w >= 2 ** 31 // max(ci, co):
+        raise ValueError("tensor too large for 32-bit pixel indexing")
+    for t, shp, name in ((out, (n, h, w, co), "out"), (pooled, (n, h // 2, w // 2, co), "pooled")):
+        if t is not None:
+            if tuple(t.shape) != shp:
+                raise ValueError(f"{name} must be {list(shp)}")
+            _check_act(t, name, dtype=dt)
+    if out is None:
+        out = torch.empty(n, h, w, co, dtype=dt, device=x.device)
+    if pooled is None:
+        pooled = torch.empty(n, h // 2, w // 2, co, dtype=dt, device=x.device)
+    C.conv_pool_fwd(x.data_ptr(), wpack.data_ptr(), bias.data_ptr(), out.data_ptr(), pooled.data_ptr(), n, h, w, ci,
+                    co, ksize, dil, tile, dt_code(dt), _ext.stream_ptr(x.device))
+    return out, pooled
+
+
 def conv_f1(x: Optional[torch.Tensor], wpack: torch.Tensor, bias: Optional[torch.Tensor], img: torch.Tensor,
             w1pack: torch.Tensor, b1: torch.Tensor, *, epi: int) -> torch.Tensor:
     """epi=EPI_BIAS_RELU: conv1_2 forward, relu(conv(X2, wpack) + bias) with X2 recomputed from img (x unused).

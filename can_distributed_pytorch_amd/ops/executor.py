@@ -189,6 +189,12 @@ class CANNetExecutor:
         fwd, _ = self.packs[id(s.module.weight)]
         return C.conv_igemm(x, fwd, s.module.bias.detach(), ksize=s.ksize, dil=s.dil, epi=epi, first=s.first)
 
+    def _pool_fused(self, s: ConvSpec, x) -> bool:
+        """The 2x2 max-pool after this conv runs in the conv's epilogue (LDS-DMA kernels; the Cin = 64 layer
+        keeps its halo kernel + separate pool).  CANNET_POOL_FWD_FUSED=0: separate pool kernel."""
+        return (s.pool_after and not s.first and s.cin != 64 and os.environ.get("CANNET_POOL_FWD_FUSED", "1") != "0"
+                and C.conv_pool_fwd_ok(x, s.cout, s.ksize))
+
     def _maxpool(self, x):
         n, h, w, c = x.shape
         y = torch.empty(n, h // 2, w // 2, c, dtype=self.act, device=x.device)
@@ -242,6 +248,11 @@ class CANNetExecutor:
                 w1, b1 = self._f1_args()
                 fwd, _ = self.packs[id(s.module.weight)]
                 y = C.conv_f1(None, fwd, s.module.bias.detach(), acts[0], w1, b1, epi=C.EPI_BIAS_RELU)
+            elif self._pool_fused(s, x):
+                fwd, _ = self.packs[id(s.module.weight)]
+                y, x = C.conv_pool_fwd(x, fwd, s.module.bias.detach(), ksize=s.ksize, dil=s.dil)
+                pre_pool[s.idx] = y
+                continue
             else:
                 y = self._conv(s, x)
             if s.pool_after:

@@ -207,6 +207,28 @@ def test_conv_wgrad_v2_half_tiles(n, h, w, ci, co, dil, cfg, bias):
         _close(db, gb, 1e-2)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("n,h,w,ci,co,dil", [(2, 8, 512, 128, 128, 1), (1, 6, 256, 256, 256, 1),
+                                             (2, 4, 256, 256, 128, 2), (1, 4, 512, 128, 64, 1)])
+def test_conv_pool_fwd_fused(n, h, w, ci, co, dil, dtype):
+    """conv + bias + ReLU with the 2x2 max-pool in the epilogue == conv_igemm(EPI_BIAS_RELU) + max_pool2d, bitwise
+    (both outputs; the 2-row pixel tiling must not change any conv value)."""
+    from can_distributed_pytorch_amd.ops import conv as C
+    torch.manual_seed(12)
+    x = torch.randn(n, h, w, ci, device="cuda").to(dtype)
+    wt = torch.randn(co, ci, 3, 3, device="cuda") * (2.0 / (9 * ci)) ** 0.5
+    b = torch.randn(co, device="cuda") * 0.1
+    wp = C.pack_weight_fwd(wt, dtype)
+    assert C.conv_pool_fwd_ok(x, co, 3)
+    y, yp = C.conv_pool_fwd(x, wp, b, ksize=3, dil=dil)
+    y_ref = C.conv_igemm(x, wp, b, ksize=3, dil=dil)
+    yp_ref = F.max_pool2d(y_ref.permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1).contiguous()
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_ref)
+    assert torch.equal(yp, yp_ref)
+    assert not C.conv_pool_fwd_ok(x[:, :h - 1].contiguous(), co, 3)     # odd H: not covered
+
+
 @pytest.mark.parametrize("n,h,w,ci,co,dil,beta", [(2, 8, 64, 512, 256, 2, 0.0), (1, 6, 128, 1024, 512, 1, 1.0),
                                                     (2, 5, 64, 256, 512, 2, 0.5)])
 def test_wgrad_tiled_reduction_matches_grid_stride(n, h, w, ci, co, dil, beta, monkeypatch):
