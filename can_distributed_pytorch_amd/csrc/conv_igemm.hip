@@ -756,6 +756,9 @@ struct HaloConvArgs {
   const bf16_t* img = nullptr;
   const bf16_t* w1 = nullptr;
   const float* b1 = nullptr;
+  // EPI_POOLFWD (CO = 64, TCOL = 64; H % 4 == 0, W % 64 == 0): the 2x2/s2 max-pool of the output tile
+  // -> yp [N][H/2][W/2][64]
+  bf16_t* yp = nullptr;
 };
 
 template <int DT, int CO, int EPI, int TCOL, int F1 = 0>
@@ -774,6 +777,7 @@ conv_halo64_kernel(HaloConvArgs a) {
   static_assert(GW >= 1, "weights split");
   static_assert(TCOL == 128 || (TCOL == 64 && CO == 64), "tile");
   static_assert(!F1 || (CO == 64 && (EPI == EPI_BIAS_RELU || EPI == EPI_MASK)), "F1 recompute: conv1_2 fwd/dgrad");
+  static_assert(EPI != EPI_POOLFWD || (CO == 64 && TCOL == 64 && !F1), "fused pool: conv1_2 64-column tiles");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* halo = smem;
@@ -916,10 +920,13 @@ conv_halo64_kernel(HaloConvArgs a) {
 
   // ---- epilogue: lane owns 16 consecutive channels of one pixel per fragment
   const int oh = oh0 + r;
+  // fused pool: every wave's tap reads are done before the halo region becomes the output staging tile
+  // (the host guarantees full tiles, so no wave leaves before the barriers)
+  if constexpr (EPI == EPI_POOLFWD) __syncthreads();
   if (oh >= a.H) return;
   const int chb = wc * 64 + fq * 16;
   float bias[16];
-  if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS || (F1 && EPI == EPI_MASK)) {
+  if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS || EPI == EPI_POOLFWD || (F1 && EPI == EPI_MASK)) {
     const float* bsrc = (F1 && EPI == EPI_MASK) ? a.b1 : a.bias;   // F1 mask: conv1_1's bias
 #pragma unroll
     for (int c = 0; c < 16; c += 4) {
@@ -974,10 +981,44 @@ conv_halo64_kernel(HaloConvArgs a) {
         v[c] = pos ? v[c] : 0.f;
       }
     }
-    *reinterpret_cast<uint4*>(a.y + off) =
+    const uint4 o0 =
         make_uint4(pack2<DT>(v[0], v[1]), pack2<DT>(v[2], v[3]), pack2<DT>(v[4], v[5]), pack2<DT>(v[6], v[7]));
-    *reinterpret_cast<uint4*>(a.y + off + 8) =
+    const uint4 o1 =
         make_uint4(pack2<DT>(v[8], v[9]), pack2<DT>(v[10], v[11]), pack2<DT>(v[12], v[13]), pack2<DT>(v[14], v[15]));
+    *reinterpret_cast<uint4*>(a.y + off) = o0;
+    *reinterpret_cast<uint4*>(a.y + off + 8) = o1;
+    if constexpr (EPI == EPI_POOLFWD) {
+      // staging tile [4 rows][64 cols] x 128 B, 16-B chunk c of column col at slot c ^ (col & 7)
+      const int col = i * 16 + fr;
+      uint4* st = reinterpret_cast<uint4*>(halo + (r * 64 + col) * 128);
+      st[(2 * fq) ^ (col & 7)] = o0;
+      st[(2 * fq + 1) ^ (col & 7)] = o1;
+    }
+  }
+  if constexpr (EPI == EPI_POOLFWD) {
+    __syncthreads();
+    // 2 pooled rows x 32 pooled columns x 8 chunks of 8 channels: 512 outputs, 2 per thread; max of the
+    // stored (rounded) values, exactly what maxpool_fwd_kernel computes from the stored map
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int o = tid + 256 * u;
+      const int c = o & 7, pc = (o >> 3) & 31, pr = o >> 8;
+      float m[8], t[8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int rr = 2 * pr + (q >> 1), cc = 2 * pc + (q & 1);
+        const uint4 v4 = reinterpret_cast<const uint4*>(halo + (rr * 64 + cc) * 128)[c ^ (cc & 7)];
+        if (q == 0) {
+          unpack8h<DT>(v4, m);
+        } else {
+          unpack8h<DT>(v4, t);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) m[k] = fmaxf(m[k], t[k]);
+        }
+      }
+      const size_t po = ((size_t)(n * (a.H >> 1) + (oh0 >> 1) + pr) * (a.W >> 1) + (ow0 >> 1) + pc) * 64 + c * 8;
+      *reinterpret_cast<uint4*>(a.yp + po) = pack8h<DT>(m);
+    }
   }
 }
 
@@ -1224,6 +1265,16 @@ template <int DT>
 static int conv_pool_fwd_impl(const void* x, const void* w, const float* bias, void* y, void* yp, int N, int H,
                               int W, int Cin, int Cout, int ksize, int dil, int tile_cfg, hipStream_t s) {
   if (Cout % 64 || Cin % 64 || H < 2 || W < 2) return -3;
+  if (Cin == 64 && Cout == 64 && ksize == 3 && dil == 1 && tile_cfg == 0) {
+    // conv1_2: halo-tiled kernel, 4 x 64 output tiles (full tiles only: the pool epilogue has barriers)
+    if (H % 4 || W % 64) return -13;
+    HaloConvArgs h;
+    h.x = (const bf16_t*)x; h.w = (const bf16_t*)w; h.bias = bias; h.mask = nullptr; h.y = (bf16_t*)y;
+    h.yp = (bf16_t*)yp; h.zero = conv_zero_page();
+    if (!h.zero) return -10;
+    h.N = N; h.H = H; h.W = W; h.tiles_x = W / 64; h.tiles_y = H / 4;
+    return launch_halo64<DT, 64, EPI_POOLFWD, 64>(h, s);
+  }
   ConvArgs2 b;
   b.x = (const bf16_t*)x; b.w = (const bf16_t*)w; b.bias = bias; b.mask = nullptr; b.y = (bf16_t*)y;
   b.yp = (bf16_t*)yp; b.zero = conv_zero_page();
@@ -1273,5 +1324,6 @@ extern "C" int can_conv_pool_fwd(const void* x, const void* w, const float* bias
 // pixels per tile of the kernel conv_pool_fwd runs for this layer (tile_cfg 0 = default): the fused pool
 // needs H even and W % (tp / 2) == 0
 extern "C" int can_conv_pool_tp(int Cin, int Cout, int ksize, int tile_cfg) {
+  if (Cin == 64 && Cout == 64 && ksize == 3 && tile_cfg == 0) return 128;   // halo kernel: W % 64 (and H % 4)
   return can::glds_cfg_tp(tile_cfg ? tile_cfg : can::glds_default_cfg(Cin, Cout, ksize));
 }

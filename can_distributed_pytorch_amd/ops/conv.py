@@ -256,6 +256,8 @@ def conv_pool_fwd_ok(x: torch.Tensor, cout: int, ksize: int, tile: int = 0) -> b
     n, h, w, ci = x.shape
     if ci % 64 or cout % 64 or h % 2 or h < 2 or w < 2:
         return False
+    if ci == 64 and cout == 64 and ksize == 3 and tile == 0 and h % 4:
+        return False                       # conv1_2's halo kernel pools whole 4-row tiles
     tp = _ext.require().conv_pool_tp(ci, cout, ksize, tile)
     return tp > 0 and w % (tp // 2) == 0
 

@@ -190,10 +190,10 @@ class CANNetExecutor:
         return C.conv_igemm(x, fwd, s.module.bias.detach(), ksize=s.ksize, dil=s.dil, epi=epi, first=s.first)
 
     def _pool_fused(self, s: ConvSpec, x) -> bool:
-        """The 2x2 max-pool after this conv runs in the conv's epilogue (LDS-DMA kernels; the Cin = 64 layer
-        keeps its halo kernel + separate pool).  CANNET_POOL_FWD_FUSED=0: separate pool kernel."""
-        return (s.pool_after and not s.first and s.cin != 64 and os.environ.get("CANNET_POOL_FWD_FUSED", "1") != "0"
-                and C.conv_pool_fwd_ok(x, s.cout, s.ksize))
+        """The 2x2 max-pool after this conv runs in the conv's epilogue (LDS-DMA kernels; conv1_2: the halo
+        kernel's epilogue through an LDS staging tile).  CANNET_POOL_FWD_FUSED=0: separate pool kernel."""
+        return (s.pool_after and not s.first and s.dil == 1 and (s.cin != 64 or s.cout == 64)
+                and os.environ.get("CANNET_POOL_FWD_FUSED", "1") != "0" and C.conv_pool_fwd_ok(x, s.cout, s.ksize))
 
     def _maxpool(self, x):
         n, h, w, c = x.shape

@@ -209,7 +209,8 @@ def test_conv_wgrad_v2_half_tiles(n, h, w, ci, co, dil, cfg, bias):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("n,h,w,ci,co,dil", [(2, 8, 512, 128, 128, 1), (1, 6, 256, 256, 256, 1),
-                                             (2, 4, 256, 256, 128, 2), (1, 4, 512, 128, 64, 1)])
+                                             (2, 4, 256, 256, 128, 2), (1, 4, 512, 128, 64, 1),
+                                             (2, 8, 128, 64, 64, 1), (1, 12, 320, 64, 64, 1)])
 def test_conv_pool_fwd_fused(n, h, w, ci, co, dil, dtype):
     """conv + bias + ReLU with the 2x2 max-pool in the epilogue == conv_igemm(EPI_BIAS_RELU) + max_pool2d, bitwise
     (both outputs; the 2-row pixel tiling must not change any conv value)."""
@@ -227,6 +228,9 @@ def test_conv_pool_fwd_fused(n, h, w, ci, co, dil, dtype):
     assert torch.equal(y, y_ref)
     assert torch.equal(yp, yp_ref)
     assert not C.conv_pool_fwd_ok(x[:, :h - 1].contiguous(), co, 3)     # odd H: not covered
+    if ci == 64 and co == 64:                                            # halo kernel: whole 4-row tiles
+        assert not C.conv_pool_fwd_ok(x[:, :h - 2].contiguous(), co, 3)
+        assert not C.conv_pool_fwd_ok(x[:, :, :w - 32].contiguous(), co, 3)
 
 
 @pytest.mark.parametrize("n,h,w,ci,co,dil,beta", [(2, 8, 64, 512, 256, 2, 0.0), (1, 6, 128, 1024, 512, 1, 1.0),
