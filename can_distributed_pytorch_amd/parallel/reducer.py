@@ -42,8 +42,14 @@ class Bucket:
 
 
 def plan_buckets(arena: FlatArena, ready_order: Sequence[int], bucket_mb: float = 25.0,
-                 first_bucket_mb: float = 1.0) -> List[Bucket]:
-    """Greedy bucketing over the arena in ready order (arena must follow that order)."""
+                 first_bucket_mb: float = 1.0, last_bucket_mb: Optional[float] = 1.0) -> List[Bucket]:
+    """Greedy bucketing over the arena in ready order (arena must follow that order).
+
+    Like DDP: a small first bucket (its all-reduce starts early) and ``bucket_mb`` caps.  Unlike DDP the
+    TAIL is split too: the trailing parameters (conv1_2 / conv1_1, whose weight gradients finish last)
+    form their own bucket of at most ``last_bucket_mb``, so the ~11 MiB of frontend gradients before them
+    are all-reduced while those last weight gradients still run, and only a ~150 KiB all-reduce is
+    exposed after the backward (None: DDP's greedy tail)."""
     slots = [arena.slot(i) for i in ready_order]
     for (s0, e0), (s1, _) in zip(slots, slots[1:]):
         if s1 != e0:
@@ -62,14 +68,26 @@ def plan_buckets(arena: FlatArena, ready_order: Sequence[int], bucket_mb: float 
             cap = bucket_mb * MIB
     if cur:
         buckets.append(Bucket(cur_start, slots[-1][1], cur))
+    last = buckets[-1]
+    if last_bucket_mb is not None and len(last.params) > 1 and last.numel * 4 > last_bucket_mb * MIB:
+        k = len(last.params) - 1            # first index of the tail: at least one parameter
+        while k > 1:
+            s0 = arena.slot(last.params[k - 1])[0]
+            if (last.end - s0) * 4 > last_bucket_mb * MIB:
+                break
+            k -= 1
+        split = arena.slot(last.params[k])[0]
+        buckets[-1] = Bucket(last.start, split, last.params[:k])
+        buckets.append(Bucket(split, last.end, last.params[k:]))
     return buckets
 
 
 class BucketedReducer:
     def __init__(self, arena: FlatArena, ready_order: Sequence[int], bucket_mb: float = 25.0,
-                 first_bucket_mb: float = 1.0, transport: str = "auto", group=None, comm=None):
+                 first_bucket_mb: float = 1.0, transport: str = "auto", group=None, comm=None,
+                 last_bucket_mb: Optional[float] = 1.0):
         self.arena = arena
-        self.buckets = plan_buckets(arena, ready_order, bucket_mb, first_bucket_mb)
+        self.buckets = plan_buckets(arena, ready_order, bucket_mb, first_bucket_mb, last_bucket_mb)
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         dev = arena.grad.device

@@ -102,14 +102,14 @@ def test_adaptive_bins_overlap_like_survey():
 @settings(max_examples=60, deadline=None)
 @given(sizes=st.lists(st.integers(1, 400_000), min_size=1, max_size=40),
        cap=st.sampled_from([0.25, 1.0, 4.0]), first=st.sampled_from([0.05, 0.5, 1.0]),
-       seed=st.integers(0, 1000))
-def test_plan_buckets_properties(sizes, cap, first, seed):
+       seed=st.integers(0, 1000), last=st.sampled_from([None, 0.1, 1.0]))
+def test_plan_buckets_properties(sizes, cap, first, seed, last):
     from can_distributed_pytorch_amd.utils.flat import FlatArena
     from can_distributed_pytorch_amd.parallel.reducer import plan_buckets, MIB
     params = [torch.nn.Parameter(torch.zeros(n)) for n in sizes]
     order = torch.randperm(len(sizes), generator=torch.Generator().manual_seed(seed)).tolist()
     arena = FlatArena(params, "cpu", order=order)
-    bks = plan_buckets(arena, order, bucket_mb=cap, first_bucket_mb=first)
+    bks = plan_buckets(arena, order, bucket_mb=cap, first_bucket_mb=first, last_bucket_mb=last)
     # every parameter exactly once, in ready order, buckets contiguous and covering the arena
     assert [i for b in bks for i in b.params] == order
     assert bks[0].start == 0 and bks[-1].end == arena.numel
@@ -119,11 +119,20 @@ def test_plan_buckets_properties(sizes, cap, first, seed):
     for b in bks:
         assert b.numel == sum(padded[i] for i in b.params)
         assert all(padded[i] >= sizes[i] and padded[i] % 64 == 0 for i in b.params)
-    # every bucket but the last reached its cap, and dropping its last parameter would not have
-    caps = [first] + [cap] * (len(bks) - 1)
-    for b, c in zip(bks[:-1], caps):
+    # greedy part: every bucket but the tail reached its cap, and dropping its last parameter would not have
+    greedy = plan_buckets(arena, order, bucket_mb=cap, first_bucket_mb=first, last_bucket_mb=None)
+    caps = [first] + [cap] * (len(greedy) - 1)
+    for b, c in zip(greedy[:-1], caps):
         assert b.numel * 4 >= c * MIB
         assert (b.numel - padded[b.params[-1]]) * 4 < c * MIB
+    assert [b.params for b in bks[:len(greedy) - 1]] == [b.params for b in greedy[:-1]]
+    # tail split: the greedy tail becomes (head, tail) with the tail <= last cap (or one parameter)
+    if last is not None and len(bks) == len(greedy) + 1:
+        assert bks[-2].params + bks[-1].params == greedy[-1].params
+        assert bks[-1].numel * 4 <= last * MIB or len(bks[-1].params) == 1
+        assert len(bks[-2].params) >= 1
+    else:
+        assert len(bks) == len(greedy)
 
 
 # --------------------------------------------------------------------------- distributed MAE normalisation
