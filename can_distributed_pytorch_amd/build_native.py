@@ -91,7 +91,7 @@ def _compile(src: str, headers, verbose=False, asan: bool = False) -> str:
 
 def build(jobs: int = 8, verbose: bool = False, asan: bool = False) -> str:
     os.makedirs(BUILD + ("_asan" if asan else ""), exist_ok=True)
-    headers = glob.glob(os.path.join(CSRC, "*.h"))
+    headers = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(CSRC, "*.inc"))
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         objs = list(ex.map(lambda s: _compile(s, headers, verbose, asan), srcs))

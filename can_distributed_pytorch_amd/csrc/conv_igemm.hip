@@ -894,9 +894,11 @@ conv_halo64_kernel(HaloConvArgs a) {
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
     // tap t's weights (and, for t = 0, the halo) have landed; the ring slot of
-    // tap t-1 is free once every wave is past this barrier
-    if (t + 1 < 9) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" :: "n"(GW) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    // tap t-1 is free once every wave is past this barrier WITH its tap t-1 LDS
+    // reads completed (lgkmcnt(0)): an issued-but-unreturned ds_read of the slot
+    // can otherwise be overtaken by the tap t+2 DMA another wave issues next
+    if (t + 1 < 9) asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" :: "n"(GW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (t + 2 < 9) issue_w(t + 2);
     const int kh = t / 3, kw = t % 3;
     const unsigned char* Ab = wring + (t % 3) * WTAP;

@@ -1040,6 +1040,8 @@ static int launch_halo(HaloArgs& a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+#include "wgrad_ring.inc"
+
 template <int DT, int WC, int WK, int WM, bool FIRST>
 static int launch_wgrad(const WgradArgs& a, hipStream_t s) {
   constexpr int TCo = 64 * WC, TK = 64 * WK;
@@ -1360,9 +1362,15 @@ static int conv_wgrad_impl(const void* dy, const void* x, float* ws, float* wsb,
       HaloArgs h;
       h.dy = a.dy; h.x = a.x; h.zero = a.zero; h.ws = ws; h.wsb = wsb_used;
       h.N = N; h.H = H; h.W = W; h.Cin = Cin; h.Cout = Cout; h.K = K; h.S = S;
-      h.tiles_y = (H + 1) / 2; h.tiles_x = (W + 63) / 64; h.ntiles = N * h.tiles_y * h.tiles_x;
+      // Cout = 128 runs as two 64-channel co tiles.  Default: the row-ring kernel (4-row tiles walked
+      // down 64-column strips, each input row fetched once per strip); CANNET_WGRAD_RING=0: 2-row tiles
+      // with a full halo per tile
+      const char* ring_env = getenv("CANNET_WGRAD_RING");
+      const bool ring = ring_env == nullptr || atoi(ring_env) != 0;
+      const int th = ring ? 4 : 2;
+      h.tiles_y = (H + th - 1) / th; h.tiles_x = (W + 63) / 64; h.ntiles = N * h.tiles_y * h.tiles_x;
       h.tiles_per_slice = (h.ntiles + S - 1) / S;
-      rc = launch_halo<DT, 64, 2>(h, s);   // Cout = 128 runs as two 64-channel co tiles
+      rc = ring ? launch_halo_ring<DT, 64, 4>(h, s) : launch_halo<DT, 64, 2>(h, s);
       if (rc) return rc;
       const int plane = K * Cout;
       return launch_reduce2(ws, wsb_used, dw, db, S, S, K, Cout, Cin, 9, 0, beta, scale, dscale, s);

@@ -146,11 +146,15 @@ def test_conv_wgrad_first_layer():
     _close(db, gb, 1e-2)
 
 
+@pytest.mark.parametrize("ring", ["1", "0"])
 @pytest.mark.parametrize("n,h,w,ci,co", [(1, 256, 1024, 64, 64), (2, 181, 733, 128, 128), (1, 301, 900, 64, 128)])
-def test_conv_wgrad_halo_path(n, h, w, ci, co):
-    """Large-M, small-channel layers take the halo-tiled wgrad kernel (odd H, W not a multiple of 64 included)."""
+def test_conv_wgrad_halo_path(n, h, w, ci, co, ring, monkeypatch):
+    """Large-M, small-channel layers take the halo-tiled wgrad kernel (odd H, W not a multiple of 64 included).
+    ring=1 (default): row-ring kernel, 4-row tiles down 64-column strips; the last two shapes have slices that
+    cross strip boundaries (full-halo reload mid-slice) and a ragged last tile row."""
     from can_distributed_pytorch_amd.ops import _ext
     from can_distributed_pytorch_amd.ops import conv as C
+    monkeypatch.setenv("CANNET_WGRAD_RING", ring)
     assert _ext.require().wgrad_plan(n * h * w, ci, co, 3, 0, 1024)[2] == 8
     torch.manual_seed(5)
     x = torch.randn(n, h, w, ci, device="cuda").to(torch.bfloat16)
@@ -283,10 +287,12 @@ def test_conv_dgrad_pool_backward_fused(n, h, w, ci, co, dtype):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("n,h,w", [(2, 40, 136), (1, 301, 900)])
-def test_conv1_2_with_conv1_1_recomputed_is_bitwise_stored_path(n, h, w, dtype):
+def test_conv1_2_with_conv1_1_recomputed_is_bitwise_stored_path(n, h, w, dtype, monkeypatch):
     """conv1_2 fwd / dgrad / wgrad with conv1_1's output recomputed from the image == the stored-X2 path, bitwise
-    (same MFMA K order for conv1_1, same rounding)."""
+    (same MFMA K order for conv1_1, same rounding).  The stored-path weight gradient runs on the 2-row halo
+    kernel here (CANNET_WGRAD_RING=0): the recompute kernel shares its tile order, the row-ring kernel does not."""
     from can_distributed_pytorch_amd.ops import conv as C
+    monkeypatch.setenv("CANNET_WGRAD_RING", "0")
     torch.manual_seed(10)
     img = torch.randn(n, 3, h, w, device="cuda")
     x4 = C.to_nhwc4(img, dtype)
