@@ -28,6 +28,7 @@ re-designed for MI355X:
 """
 from __future__ import annotations
 
+import contextlib
 from typing import Optional
 
 import torch
@@ -104,12 +105,17 @@ class NativeStepper:
         if red is not None:
             red.begin()
             red.mark_ready([ex.head_w_index, ex.head_b_index])
+        # scalars: [nonfinite flag, loss].  Issued on the weight-gradient side stream, idle at this point,
+        # so the handful of tiny kernels stay off the step's tail; backward_features joins that stream
+        side = ex._side_stream()
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            self.flags[0:1].copy_((~torch.isfinite(loss)).float())
+            self.flags[1:2].copy_(loss)
         ex.backward_features(sv, d_b6, self.grads, on_grad_ready=(red.mark_ready if red is not None else None),
                              dscale=sc[1:2] if sc is not None else None)
         del sv
-        # scalars: [nonfinite flag, loss]
-        self.flags[0:1].copy_((~torch.isfinite(loss)).float())
-        self.flags[1:2].copy_(loss)
         if red is not None:
             red.finish()
             red.allreduce_scalars(self.flags[0:2])
