@@ -38,9 +38,9 @@ int can_maxpool_bwd_relu(const void* x, const void* dy, void* dx, int N, int H, 
 int can_head_fwd(const void* y, const float* w, const float* b, float* et, int P, int dt, void* stream);
 int can_head_train(const void* y, const float* w, const float* b, const float* gt, float* et, void* dy, float* part,
                    int nblk, float* dw, float* db, float* loss, int P, float gscale, float beta, const float* lscale,
-                   int dt, void* stream);
+                   float* nonfinite, int dt, void* stream);
 int can_sgd_momentum(float* p, float* buf, const float* g, size_t n, float lr, float momentum, float gscale,
-                     int first, const float* flags, void* stream);
+                     int first, float* flags, const float* lr_dev, void* stream);
 int can_grad_nonfinite(const float* g, size_t n, float* flags, void* stream);
 int can_scale_update(const float* flags, float* scaler, int interval, float growth, float backoff, float max_scale,
                      void* stream);
@@ -56,6 +56,8 @@ int can_ctx_fuse(const void* fv, const void* ws, const float* T, void* cat, int 
                  void* stream);
 int can_ctx_bwd_e1(const void* dcat, const void* ws, const float* T, void* dz, void* sdir, int N, int h, int w, int C,
                    int dt, void* stream);
+int can_ctx_gemm(int mode, const float* x, const float* y, const float* const* w, float* out, float* const* gw, int N,
+                 int C, float beta, float scale, const float* dscale, void* stream);
 int can_ctx_bwd_final(const void* dcat, const void* dc, const float* dave, const void* fv, void* dfv, int N, int h,
                       int w, int C, int dt, void* stream);
 

@@ -104,16 +104,16 @@ PYBIND11_MODULE(CAN_MODULE_NAME, m) {
   });
   m.def("head_train", [](uintptr_t y, uintptr_t w, uintptr_t b, uintptr_t gt, uintptr_t et, uintptr_t dy,
                          uintptr_t part, int nblk, uintptr_t dw, uintptr_t db, uintptr_t loss, int Pn, float gscale,
-                         float beta, uintptr_t lscale, int dt, uintptr_t st) {
+                         float beta, uintptr_t lscale, uintptr_t nonfinite, int dt, uintptr_t st) {
     check(can_head_train(P(y), (const float*)w, (const float*)b, (const float*)gt, (float*)et, P(dy), (float*)part,
-                         nblk, (float*)dw, (float*)db, (float*)loss, Pn, gscale, beta, (const float*)lscale, dt,
-                         P(st)),
+                         nblk, (float*)dw, (float*)db, (float*)loss, Pn, gscale, beta, (const float*)lscale,
+                         (float*)nonfinite, dt, P(st)),
           "head_train");
   });
   m.def("sgd_momentum", [](uintptr_t p, uintptr_t buf, uintptr_t g, size_t n, float lr, float mom, float gscale,
-                           int first, uintptr_t flags, uintptr_t st) {
-    check(can_sgd_momentum((float*)p, (float*)buf, (const float*)g, n, lr, mom, gscale, first, (const float*)flags,
-                           P(st)),
+                           int first, uintptr_t flags, uintptr_t lr_dev, uintptr_t st) {
+    check(can_sgd_momentum((float*)p, (float*)buf, (const float*)g, n, lr, mom, gscale, first, (float*)flags,
+                           (const float*)lr_dev, P(st)),
           "sgd_momentum");
   });
   m.def("grad_nonfinite", [](uintptr_t g, size_t n, uintptr_t flags, uintptr_t st) {
@@ -150,6 +150,17 @@ PYBIND11_MODULE(CAN_MODULE_NAME, m) {
   m.def("ctx_bwd_e1", [](uintptr_t dcat, uintptr_t ws, uintptr_t T, uintptr_t dz, uintptr_t sdir, int N, int h, int w,
                          int C, int dt, uintptr_t st) {
     check(can_ctx_bwd_e1(P(dcat), P(ws), (const float*)T, P(dz), P(sdir), N, h, w, C, dt, P(st)), "ctx_bwd_e1");
+  });
+  m.def("ctx_gemm", [](int mode, uintptr_t x, uintptr_t y, std::vector<uintptr_t> w, uintptr_t out,
+                       std::vector<uintptr_t> gw, int N, int C, float beta, float scale, uintptr_t dscale, uintptr_t st) {
+    if ((!w.empty() && w.size() != 4) || (!gw.empty() && gw.size() != 4)) throw std::runtime_error("ctx_gemm: 4 scales");
+    const float* wp[4] = {nullptr, nullptr, nullptr, nullptr};
+    float* gp[4] = {nullptr, nullptr, nullptr, nullptr};
+    for (size_t i = 0; i < w.size(); ++i) wp[i] = (const float*)w[i];
+    for (size_t i = 0; i < gw.size(); ++i) gp[i] = (float*)gw[i];
+    check(can_ctx_gemm(mode, (const float*)x, (const float*)y, wp, (float*)out, gp, N, C, beta, scale,
+                       (const float*)dscale, P(st)),
+          "ctx_gemm");
   });
   m.def("ctx_bwd_final", [](uintptr_t dcat, uintptr_t dc, uintptr_t dave, uintptr_t fv, uintptr_t dfv, int N, int h,
                             int w, int C, int dt, uintptr_t st) {

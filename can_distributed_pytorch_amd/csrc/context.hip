@@ -452,6 +452,107 @@ __global__ void __launch_bounds__(256) ctx_bwd_final_kernel(const uint4* __restr
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// conv{S}_1 (1x1, 512->512, no bias) on the pooled S x S grids, all four
+// scales in ONE launch (blockIdx.z = scale), fp32 (model/CANNet.py:43,52,61,72;
+// SURVEY §2.5 X2).  Cells are [N][50][C] fp32 (scale S at cell offset
+// {0,1,5,14}, S*S cells per image); weights are the fp32 masters [C][C]
+// (out, in).  Three GEMM shapes, out[m][n] = sum_k X(m,k) Y(k,n):
+//   MODE 0 forward        table[r][o] = sum_k ave[r][k] * W[o][k]       (m = cell row r)
+//   MODE 1 data gradient  dave[r][i]  = sum_o dA[r][o]  * W[o][i]
+//   MODE 2 weight grad    dW[o][i]    = sum_r dA[r][o]  * ave[r][i]     (k = cell row r)
+// 32 x 64 output tiles, 256 threads x (2 x 4) outputs, K tiles of 32 staged in
+// LDS; fixed summation order (deterministic).  M <= 288 rows at batch 8: the
+// whole context GEMM work is ~0.2 GFLOP, so this is a launch-count kernel
+// (replaces 12 hipBLASLt GEMMs + 4 copies per step), not an MFMA one.
+struct CtxGemmArgs {
+  const float* x;        // MODE 0/1: cells (ave / dA); MODE 2: dA
+  const float* y;        // MODE 2: ave
+  const float* w[4];     // MODE 0/1: W1 per scale
+  float* out;            // MODE 0/1: cells (table / dave)
+  float* gw[4];          // MODE 2: dW1 per scale
+  int N, C;
+  float beta, scale;
+  const float* dscale;
+};
+
+__device__ __forceinline__ int ctx_cell_row(int r, int k2, int off) { return (r / k2) * 50 + off + (r % k2); }
+
+template <int MODE>
+__global__ void __launch_bounds__(256) ctx_gemm_kernel(CtxGemmArgs a) {
+  constexpr int TM = 32, TN = 64, TK = 32;
+  __shared__ float Xs[TK][TM + 1];
+  __shared__ float Ys[TK][TN + 4];
+  const int si = blockIdx.z;
+  const int S = (si == 0) ? 1 : (si == 1) ? 2 : (si == 2) ? 3 : 6;
+  const int off = (si == 0) ? 0 : (si == 1) ? 1 : (si == 2) ? 5 : 14;
+  const int k2 = S * S, R = a.N * k2, C = a.C;
+  const int M = (MODE == 2) ? C : R, K = (MODE == 2) ? R : C;
+  const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TN;
+  if (m0 >= M) return;
+  const float* W = a.w[si];
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  float acc[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  for (int k0 = 0; k0 < K; k0 += TK) {
+    for (int e = tid; e < TM * TK; e += 256) {
+      int mm, kk;
+      if (MODE == 2) { mm = e % TM; kk = e / TM; }   // dA[row(k)][m]: m contiguous
+      else { kk = e % TK; mm = e / TK; }             // cells[row(m)][k]: k contiguous
+      const int m = m0 + mm, k = k0 + kk;
+      float v = 0.f;
+      if (m < M && k < K) {
+        if (MODE == 2) v = a.x[(size_t)ctx_cell_row(k, k2, off) * C + m];
+        else v = a.x[(size_t)ctx_cell_row(m, k2, off) * C + k];
+      }
+      Xs[kk][mm] = v;
+    }
+    for (int e = tid; e < TK * TN; e += 256) {
+      int kk, nn;
+      if (MODE == 0) { kk = e % TK; nn = e / TK; }   // W[n][k]: k contiguous
+      else { nn = e % TN; kk = e / TN; }             // W[k][n] / ave[row(k)][n]: n contiguous
+      const int k = k0 + kk, n = n0 + nn;
+      float v = 0.f;
+      if (k < K && n < C) {
+        if (MODE == 0) v = W[(size_t)n * C + k];
+        else if (MODE == 1) v = W[(size_t)k * C + n];
+        else v = a.y[(size_t)ctx_cell_row(k, k2, off) * C + n];
+      }
+      Ys[kk][nn] = v;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int kk = 0; kk < TK; ++kk) {
+      const float x0 = Xs[kk][ty * 2], x1 = Xs[kk][ty * 2 + 1];
+      const float4 y4 = *reinterpret_cast<const float4*>(&Ys[kk][tx * 4]);
+      acc[0][0] = fmaf(x0, y4.x, acc[0][0]); acc[0][1] = fmaf(x0, y4.y, acc[0][1]);
+      acc[0][2] = fmaf(x0, y4.z, acc[0][2]); acc[0][3] = fmaf(x0, y4.w, acc[0][3]);
+      acc[1][0] = fmaf(x1, y4.x, acc[1][0]); acc[1][1] = fmaf(x1, y4.y, acc[1][1]);
+      acc[1][2] = fmaf(x1, y4.z, acc[1][2]); acc[1][3] = fmaf(x1, y4.w, acc[1][3]);
+    }
+    __syncthreads();
+  }
+  const float sc = a.scale * ((a.dscale != nullptr) ? a.dscale[0] : 1.f);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = m0 + ty * 2 + i;
+    if (m >= M) continue;
+    const int n = n0 + tx * 4;
+    if (MODE == 2) {
+      float* g = a.gw[si] + (size_t)m * C + n;
+      float4 o = make_float4(acc[i][0] * sc, acc[i][1] * sc, acc[i][2] * sc, acc[i][3] * sc);
+      if (a.beta != 0.f) {
+        const float4 p = *reinterpret_cast<const float4*>(g);
+        o.x += a.beta * p.x; o.y += a.beta * p.y; o.z += a.beta * p.z; o.w += a.beta * p.w;
+      }
+      *reinterpret_cast<float4*>(g) = o;
+    } else {
+      *reinterpret_cast<float4*>(a.out + (size_t)ctx_cell_row(m, k2, off) * C + n) =
+          make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+    }
+  }
+}
+
 static inline int gridn(size_t n, int cap = 8192) {
   size_t g = (n + 255) / 256;
   if (g > (size_t)cap) g = cap;
@@ -521,5 +622,27 @@ extern "C" int can_ctx_bwd_final(const void* dcat, const void* dc, const float* 
   if (C & 7) return -2;
   CAN_LAUNCH_DT(dt, ctx_bwd_final_kernel, ctx_grid(N, h, C), dim3(256), 0, (hipStream_t)stream, (const uint4*)dcat,
                 (const uint4*)dc, dave, (const uint4*)fv, (uint4*)dfv, N, h, w, C);
+  return (int)hipGetLastError();
+}
+
+// conv{S}_1 GEMMs of all four scales in one launch.  mode 0: out = table (fwd), mode 1: out = dave,
+// mode 2: gw = dW1 per scale (beta: accumulate, scale/dscale: gradient scaling of the fp16 step).
+extern "C" int can_ctx_gemm(int mode, const float* x, const float* y, const float* const* w, float* out,
+                            float* const* gw, int N, int C, float beta, float scale, const float* dscale,
+                            void* stream) {
+  if (C % 64 != 0 || N < 1) return -2;
+  CtxGemmArgs a{};
+  a.x = x; a.y = y; a.out = out; a.N = N; a.C = C; a.beta = beta; a.scale = scale; a.dscale = dscale;
+  for (int i = 0; i < 4; ++i) {
+    a.w[i] = w ? w[i] : nullptr;
+    a.gw[i] = gw ? gw[i] : nullptr;
+  }
+  const int M = (mode == 2) ? C : N * 36;
+  const dim3 grid(C / 64, (M + 31) / 32, 4);
+  hipStream_t s = (hipStream_t)stream;
+  if (mode == 0) hipLaunchKernelGGL(ctx_gemm_kernel<0>, grid, dim3(256), 0, s, a);
+  else if (mode == 1) hipLaunchKernelGGL(ctx_gemm_kernel<1>, grid, dim3(256), 0, s, a);
+  else if (mode == 2) hipLaunchKernelGGL(ctx_gemm_kernel<2>, grid, dim3(256), 0, s, a);
+  else return -3;
   return (int)hipGetLastError();
 }

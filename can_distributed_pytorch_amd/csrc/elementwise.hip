@@ -91,9 +91,9 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(const uint4* __restrict__
   for (size_t p = ((size_t)blockIdx.x * 256 + threadIdx.x) >> 3; p < (size_t)P; p += ((size_t)gridDim.x * 256) >> 3) {
     float v[8];
     unpack8h<DT>(y[p * 8 + lane8], v);
-    float s = 0.f;
+    float s = 0.f;   // explicit fma chain: head_fwd and head_train produce bitwise-identical et
 #pragma unroll
-    for (int k = 0; k < 8; ++k) s += v[k] * wl[k];
+    for (int k = 0; k < 8; ++k) s = fmaf(v[k], wl[k], s);
     s += __shfl_xor(s, 1, 64);
     s += __shfl_xor(s, 2, 64);
     s += __shfl_xor(s, 4, 64);
@@ -122,9 +122,9 @@ __global__ void __launch_bounds__(256) head_train_kernel(const uint4* __restrict
   for (size_t p = ((size_t)blockIdx.x * 256 + threadIdx.x) >> 3; p < (size_t)P; p += ((size_t)gridDim.x * 256) >> 3) {
     float v[8];
     unpack8h<DT>(y[p * 8 + lane8], v);
-    float s = 0.f;
+    float s = 0.f;   // explicit fma chain: head_fwd and head_train produce bitwise-identical et
 #pragma unroll
-    for (int k = 0; k < 8; ++k) s += v[k] * wl[k];
+    for (int k = 0; k < 8; ++k) s = fmaf(v[k], wl[k], s);
     s += __shfl_xor(s, 1, 64);
     s += __shfl_xor(s, 2, 64);
     s += __shfl_xor(s, 4, 64);
@@ -154,9 +154,13 @@ __global__ void __launch_bounds__(256) head_train_kernel(const uint4* __restrict
 // out[0..63] = dw, out[64] = db, loss_out[0] = loss  (fixed-order, deterministic):
 // 15 groups x 66 outputs, group g sums blocks g, g+15, ... then the 15 group
 // sums are added in order (a single thread per output serialised ~1k loads).
+// nonfinite (optional): 1.0 if the loss is inf/NaN, else 0.0 -- the
+// reference's `if not isfinite(loss)` guard (utils/train_eval_utils.py:48)
+// computed where the loss is produced, no extra launch.
 __global__ void __launch_bounds__(1024) head_reduce_kernel(const float* __restrict__ part, int nblk,
                                                            float* __restrict__ dw, float* __restrict__ db,
-                                                           float* __restrict__ loss, float beta) {
+                                                           float* __restrict__ loss, float beta,
+                                                           float* __restrict__ nonfinite) {
   constexpr int G = 15;
   __shared__ float red[G][66];
   const int t = threadIdx.x;
@@ -178,21 +182,34 @@ __global__ void __launch_bounds__(1024) head_reduce_kernel(const float* __restri
     for (int q = 0; q < G; ++q) s += red[q][t];
     if (t < 64) dw[t] = (beta != 0.f) ? dw[t] * beta + s : s;
     else if (t == 64) db[0] = (beta != 0.f) ? db[0] * beta + s : s;
-    else loss[0] = s;
+    else {
+      loss[0] = s;
+      if (nonfinite != nullptr) nonfinite[0] = isfinite(s) ? 0.f : 1.f;
+    }
   }
 }
 
 // ---------------------------------------------------------------- SGD
 // torch.optim.SGD semantics (dampening 0, nesterov False, wd 0):
 //   buf = g (first step) | momentum*buf + g ;  p -= lr*buf,  g = grad*gscale.
-// flags[0] != 0 (non-finite loss) or flags[2] != 0 (non-finite gradient, set by
-// grad_nonfinite in the fp16 step) -> the whole update is skipped (graph-safe,
-// no host sync).  Vectorised float4 over a 16-B aligned arena.
+// flags = {non-finite loss (all-reduced: any rank), loss, non-finite gradient
+// (fp16 step), sticky "a non-finite loss happened since the last reset"}.
+// flags[0] != 0 or flags[2] != 0 -> the whole update is skipped (graph-safe,
+// no host sync); flags[0] != 0 also latches flags[3], which the host polls at
+// its logging cadence (a NaN on a step it does not read is never lost).
+// lr_dev (optional): the learning rate read from device memory, so a captured
+// step follows an lr schedule (the host updates the scalar between replays).
+// Vectorised float4 over a 16-B aligned arena.
 __global__ void __launch_bounds__(256) sgd_momentum_kernel(float4* __restrict__ p, float4* __restrict__ buf,
                                                            const float4* __restrict__ g, size_t n4, float lr,
                                                            float momentum, float gscale, int first,
-                                                           const float* __restrict__ flags) {
-  if (flags != nullptr && (flags[0] != 0.f || flags[2] != 0.f)) return;
+                                                           float* __restrict__ flags, const float* __restrict__ lr_dev) {
+  if (flags != nullptr) {
+    const bool bad_loss = flags[0] != 0.f;
+    if (bad_loss && blockIdx.x == 0 && threadIdx.x == 0) flags[3] = 1.f;
+    if (bad_loss || flags[2] != 0.f) return;
+  }
+  if (lr_dev != nullptr) lr = lr_dev[0];
   for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
     float4 gv = g[i];
     gv.x *= gscale; gv.y *= gscale; gv.z *= gscale; gv.w *= gscale;
@@ -361,7 +378,7 @@ extern "C" int can_head_fwd(const void* y, const float* w, const float* b, float
 
 extern "C" int can_head_train(const void* y, const float* w, const float* b, const float* gt, float* et, void* dy,
                               float* part, int nblk, float* dw, float* db, float* loss, int P, float gscale,
-                              float beta, const float* lscale, int dt, void* stream) {
+                              float beta, const float* lscale, float* nonfinite, int dt, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (dt == DT_F16)
     hipLaunchKernelGGL(head_train_kernel<DT_F16>, dim3(nblk), dim3(256), 0, s, (const uint4*)y, w, b, gt, et,
@@ -371,15 +388,15 @@ extern "C" int can_head_train(const void* y, const float* w, const float* b, con
                        (uint4*)dy, part, P, gscale, lscale);
   else
     return -20;
-  hipLaunchKernelGGL(head_reduce_kernel, dim3(1), dim3(1024), 0, s, part, nblk, dw, db, loss, beta);
+  hipLaunchKernelGGL(head_reduce_kernel, dim3(1), dim3(1024), 0, s, part, nblk, dw, db, loss, beta, nonfinite);
   return (int)hipGetLastError();
 }
 
 extern "C" int can_sgd_momentum(float* p, float* buf, const float* g, size_t n, float lr, float momentum,
-                                float gscale, int first, const float* flags, void* stream) {
+                                float gscale, int first, float* flags, const float* lr_dev, void* stream) {
   if (n & 3) return -2;
   hipLaunchKernelGGL(sgd_momentum_kernel, dim3(grid_for(n / 4, 256, 4096)), dim3(256), 0, (hipStream_t)stream,
-                     (float4*)p, (float4*)buf, (const float4*)g, n / 4, lr, momentum, gscale, first, flags);
+                     (float4*)p, (float4*)buf, (const float4*)g, n / 4, lr, momentum, gscale, first, flags, lr_dev);
   return (int)hipGetLastError();
 }
 

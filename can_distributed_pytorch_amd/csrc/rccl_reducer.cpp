@@ -31,6 +31,12 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "bucket_schedule.h"
+
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -117,21 +123,28 @@ class RcclComm {
   int rank_, world_, device_;
 };
 
+// Bucketed gradient all-reduce over RCCL.  The readiness logic lives in
+// BucketSchedule (bucket_schedule.h, shared with the CPU fake-cluster
+// transport below); this class only turns its decisions into stream work:
+//   * mark_ready(params, stream): the producing stream records one event per
+//     touched bucket (per (bucket, producer stream) slot, so a later mark on
+//     the same stream supersedes an earlier one);
+//   * a complete bucket: the comm stream waits on the events of EVERY producer
+//     stream of that bucket (compute stream and/or weight-gradient side
+//     stream), then ncclAllReduce(sum) in place on the arena slice;
+//   * finish(): launches incomplete buckets, joins the comm stream into the
+//     caller's stream with one event.  No host synchronisation anywhere.
 class BucketReducer {
  public:
   // offsets/counts in ELEMENTS of the fp32 arena; param_bucket[i] = bucket of
-  // parameter i (or -1 = not reduced); bucket_params[b] = #params in bucket b.
+  // parameter i (or -1 = not reduced).
   BucketReducer(RcclComm& comm, uintptr_t arena, std::vector<size_t> offsets, std::vector<size_t> counts,
                 std::vector<int> param_bucket, int priority)
       : comm_(comm), arena_((float*)arena), off_(std::move(offsets)), cnt_(std::move(counts)),
-        pbucket_(std::move(param_bucket)) {
+        sched_(std::move(param_bucket), (int)off_.size()) {
+    if (cnt_.size() != off_.size()) throw std::runtime_error("BucketReducer: offsets/counts size mismatch");
     const int nb = (int)off_.size();
-    total_.assign(nb, 0);
-    for (int b : pbucket_)
-      if (b >= 0) total_.at(b)++;
-    pending_ = total_;
-    launched_.assign(nb, 0);
-    ev_.resize(nb);
+    ev_.resize((size_t)nb * BucketSchedule::kMaxStreams);
     for (auto& e : ev_) hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
     hip_check(hipEventCreateWithFlags(&done_, hipEventDisableTiming), "hipEventCreate");
     int lo = 0, hi = 0;
@@ -144,56 +157,147 @@ class BucketReducer {
     hipStreamDestroy(comm_stream_);
   }
   void begin() {
-    pending_ = total_;
-    std::fill(launched_.begin(), launched_.end(), 0);
-    next_ = 0;
+    sched_.begin();
+    launched_.clear();
   }
   // Returns the number of buckets launched by this call.
-  int mark_ready(const std::vector<int>& params, uintptr_t compute_stream) {
-    for (int p : params) {
-      if (p < 0 || p >= (int)pbucket_.size()) throw std::runtime_error("mark_ready: bad param index");
-      const int b = pbucket_[p];
-      if (b < 0) continue;
-      if (--pending_[b] < 0) throw std::runtime_error("mark_ready: parameter marked twice in one step");
-    }
-    // launch full buckets strictly in bucket order (identical on every rank)
-    int n = 0;
-    while (next_ < (int)off_.size() && pending_[next_] == 0) {
-      launch(next_, (hipStream_t)compute_stream);
-      ++next_;
-      ++n;
-    }
-    return n;
+  int mark_ready(const std::vector<int>& params, uintptr_t stream) {
+    std::vector<int> touched;
+    const std::vector<int> ready = sched_.mark(params, (uint64_t)stream, &touched);
+    for (int b : touched)
+      hip_check(hipEventRecord(ev_[(size_t)b * BucketSchedule::kMaxStreams + sched_.slot_of(b, (uint64_t)stream)],
+                               (hipStream_t)stream),
+                "record bucket");
+    for (int b : ready) launch(b);
+    return (int)ready.size();
   }
   void finish(uintptr_t compute_stream) {
-    hipStream_t cs = (hipStream_t)compute_stream;
-    while (next_ < (int)off_.size()) {  // buckets holding unused params: reduce anyway
-      launch(next_, cs);
-      ++next_;
-    }
+    for (int b : sched_.finish()) launch(b);
     hip_check(hipEventRecord(done_, comm_stream_), "record done");
-    hip_check(hipStreamWaitEvent(cs, done_, 0), "wait done");
+    hip_check(hipStreamWaitEvent((hipStream_t)compute_stream, done_, 0), "wait done");
   }
   uintptr_t comm_stream() const { return (uintptr_t)comm_stream_; }
   int num_buckets() const { return (int)off_.size(); }
+  std::vector<int> launched() const { return launched_; }
 
  private:
-  void launch(int b, hipStream_t cs) {
-    hip_check(hipEventRecord(ev_[b], cs), "record bucket");
-    hip_check(hipStreamWaitEvent(comm_stream_, ev_[b], 0), "wait bucket");
+  void launch(int b) {
+    const auto& ss = sched_.streams(b);
+    for (int i = 0; i < (int)ss.size(); ++i)
+      hip_check(hipStreamWaitEvent(comm_stream_, ev_[(size_t)b * BucketSchedule::kMaxStreams + i], 0), "wait bucket");
     nccl_check(ncclAllReduce(arena_ + off_[b], arena_ + off_[b], cnt_[b], ncclFloat32, ncclSum, comm_.raw(),
                              comm_stream_),
                "bucket allreduce");
-    launched_[b] = 1;
+    launched_.push_back(b);
   }
   RcclComm& comm_;
   float* arena_;
   std::vector<size_t> off_, cnt_;
-  std::vector<int> pbucket_, total_, pending_, launched_;
+  BucketSchedule sched_;
   std::vector<hipEvent_t> ev_;
+  std::vector<int> launched_;
   hipEvent_t done_;
   hipStream_t comm_stream_;
-  int next_ = 0;
+};
+
+// ---------------------------------------------------------------------------
+// CPU fake cluster: the reducer's schedule driven by W host threads (one per
+// fake rank) with a blocking in-process SUM all-reduce as the transport.  The
+// collective checks that every rank issues the SAME sequence of (offset,
+// count) collectives — a rank that launched buckets in another order would be
+// reported as a mismatch (RCCL would hang or corrupt) — and times out instead
+// of hanging.  Used by tests/test_reducer_native.py.
+class FakeCluster {
+ public:
+  FakeCluster(int world, double timeout_s)
+      : world_(world), timeout_(timeout_s), ptr_(world, nullptr), off_(world, 0), cnt_(world, 0), in_(world, 0) {
+    if (world < 1) throw std::runtime_error("FakeCluster: world < 1");
+  }
+  void allreduce(int rank, float* base, size_t off, size_t count) {
+    std::unique_lock<std::mutex> lk(mu_);
+    if (!err_.empty()) throw std::runtime_error(err_);
+    if (in_[rank]) throw std::runtime_error("FakeCluster: rank entered a collective twice");
+    in_[rank] = 1;
+    ptr_[rank] = base;
+    off_[rank] = off;
+    cnt_[rank] = count;
+    const uint64_t gen = gen_;
+    if (++arrived_ == world_) {
+      for (int r = 1; r < world_; ++r)
+        if (off_[r] != off_[0] || cnt_[r] != cnt_[0])
+          err_ = "collective #" + std::to_string(seq_) + " mismatch: rank " + std::to_string(r) + " (" +
+                 std::to_string(off_[r]) + "," + std::to_string(cnt_[r]) + ") vs rank 0 (" + std::to_string(off_[0]) +
+                 "," + std::to_string(cnt_[0]) + ")";
+      if (err_.empty()) {
+        std::vector<double> acc(count, 0.0);
+        for (int r = 0; r < world_; ++r)
+          for (size_t i = 0; i < count; ++i) acc[i] += ptr_[r][off + i];
+        for (int r = 0; r < world_; ++r)
+          for (size_t i = 0; i < count; ++i) ptr_[r][off + i] = (float)acc[i];
+      }
+      arrived_ = 0;
+      std::fill(in_.begin(), in_.end(), 0);
+      ++seq_;
+      ++gen_;
+      cv_.notify_all();
+    } else if (!cv_.wait_for(lk, std::chrono::duration<double>(timeout_), [&] { return gen_ != gen; })) {
+      err_ = "collective #" + std::to_string(seq_) + " timed out: ranks issued different collective sequences";
+      cv_.notify_all();
+    }
+    if (!err_.empty()) throw std::runtime_error(err_);
+  }
+  int collectives() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return (int)seq_;
+  }
+
+ private:
+  int world_;
+  double timeout_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<float*> ptr_;
+  std::vector<size_t> off_, cnt_;
+  std::vector<int> in_;
+  int arrived_ = 0;
+  uint64_t gen_ = 0, seq_ = 0;
+  std::string err_;
+};
+
+// One fake rank: BucketSchedule + FakeCluster transport over a HOST fp32
+// arena.  Records, per launch, the bucket and the producer-stream tags the
+// GPU reducer would have waited on.
+class FakeRankReducer {
+ public:
+  FakeRankReducer(FakeCluster& cl, int rank, uintptr_t arena, std::vector<size_t> offsets, std::vector<size_t> counts,
+                  std::vector<int> param_bucket)
+      : cl_(cl), rank_(rank), arena_((float*)arena), off_(std::move(offsets)), cnt_(std::move(counts)),
+        sched_(std::move(param_bucket), (int)off_.size()) {}
+  void begin() {
+    sched_.begin();
+    log_.clear();
+  }
+  int mark_ready(const std::vector<int>& params, uint64_t stream) {
+    const std::vector<int> ready = sched_.mark(params, stream);
+    for (int b : ready) launch(b);
+    return (int)ready.size();
+  }
+  void finish() {
+    for (int b : sched_.finish()) launch(b);
+  }
+  std::vector<std::pair<int, std::vector<uint64_t>>> log() const { return log_; }
+
+ private:
+  void launch(int b) {
+    log_.emplace_back(b, sched_.streams(b));
+    cl_.allreduce(rank_, arena_, off_[b], cnt_[b]);
+  }
+  FakeCluster& cl_;
+  int rank_;
+  float* arena_;
+  std::vector<size_t> off_, cnt_;
+  BucketSchedule sched_;
+  std::vector<std::pair<int, std::vector<uint64_t>>> log_;
 };
 
 }  // namespace can
@@ -231,6 +335,25 @@ void register_rccl(py::module_& m) {
       .def("begin", &BucketReducer::begin)
       .def("mark_ready", &BucketReducer::mark_ready)
       .def("finish", &BucketReducer::finish)
+      .def_property_readonly("launched", &BucketReducer::launched)
       .def_property_readonly("comm_stream", &BucketReducer::comm_stream)
       .def_property_readonly("num_buckets", &BucketReducer::num_buckets);
+  py::class_<BucketSchedule>(m, "BucketSchedule")
+      .def(py::init<std::vector<int>, int>())
+      .def("begin", &BucketSchedule::begin)
+      .def("mark", [](BucketSchedule& s, const std::vector<int>& p, uint64_t stream) { return s.mark(p, stream); })
+      .def("finish", &BucketSchedule::finish)
+      .def("streams", &BucketSchedule::streams)
+      .def("pending", &BucketSchedule::pending)
+      .def_property_readonly("num_buckets", &BucketSchedule::num_buckets);
+  py::class_<FakeCluster>(m, "FakeCluster")
+      .def(py::init<int, double>())
+      .def_property_readonly("collectives", &FakeCluster::collectives);
+  py::class_<FakeRankReducer>(m, "FakeRankReducer")
+      .def(py::init<FakeCluster&, int, uintptr_t, std::vector<size_t>, std::vector<size_t>, std::vector<int>>(),
+           py::keep_alive<1, 2>())
+      .def("begin", &FakeRankReducer::begin)
+      .def("mark_ready", &FakeRankReducer::mark_ready, py::call_guard<py::gil_scoped_release>())
+      .def("finish", &FakeRankReducer::finish, py::call_guard<py::gil_scoped_release>())
+      .def("log", &FakeRankReducer::log);
 }

@@ -10,10 +10,17 @@ re-designed for MI355X:
   finished layer is handed to the bucketed reducer (parallel/reducer.py),
   which all-reduces full buckets over RCCL on a side stream while the
   remaining layers of the backward still run;
-* loss all-reduce + non-finite flag travel in one 8-byte collective;
-  averaging by 1/world is folded into the fused SGD kernel, which also skips
-  the update on a non-finite loss (the reference's sys.exit guard,
+* the loss and its non-finite flag are written by the fused head's reduction
+  kernel straight into a device flag vector, and travel in one 8-byte
+  collective; averaging by 1/world is folded into the fused SGD kernel, which
+  also skips the update on a non-finite loss and latches a sticky flag the
+  host polls at its logging cadence (the reference's sys.exit guard,
   utils/train_eval_utils.py:48-50, made device-side and graph-safe);
+* the learning rate lives in a device scalar read by the SGD kernel, so a
+  captured step follows an lr schedule;
+* roctx ranges (utils/profiling.trace_range, CANNET_ROCTX=1) mark the
+  forward / backward / all-reduce / optimizer phases; ``comm_timing`` records
+  hipEvents around the post-backward all-reduce join (exposed comm time);
 * the bf16 weight packs are refreshed by pack kernels right after SGD;
 * with ``graph=True`` the whole step (for a fixed input shape) is captured
   once into a hipGraph (torch.cuda.CUDAGraph) and replayed: one launch per
@@ -38,6 +45,7 @@ from ..models.cannet import CANNet
 from ..ops import _ext
 from ..ops.executor import CANNetExecutor
 from ..utils.flat import FlatArena
+from ..utils.profiling import trace_range
 
 ACT_DTYPES = {"bf16": torch.bfloat16, "fp16": torch.float16}
 
@@ -55,7 +63,6 @@ class NativeStepper:
         self.model = (model or CANNet(backend="hip")).to(self.device)
         self.model.exec_backend = "hip"
         self.world = world
-        self.lr = lr * world                       # train.py:25 linear scaling
         self.momentum = momentum
         self.params = list(self.model.parameters())
         self.ex = CANNetExecutor(self.model, dtype=ACT_DTYPES[dtype])
@@ -64,18 +71,25 @@ class NativeStepper:
         self.arena = FlatArena(self.params, self.device, order=self.ex.grad_ready_order())
         self.mom = torch.zeros_like(self.arena.data)  # momentum buffer (zero init == torch's first-step clone)
         self.grads = self.arena.grad_views()
-        self.flags = torch.zeros(4, dtype=torch.float32, device=self.device)   # [nonfinite loss, loss, grad overflow, 0]
+        # [non-finite loss (any rank after the all-reduce), loss, non-finite gradient (fp16), sticky non-finite]
+        self.flags = torch.zeros(4, dtype=torch.float32, device=self.device)
+        self._lr_dev = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self.lr = lr * world                       # train.py:25 linear scaling
         # fp16: device-side dynamic loss scale {S, 1/S, clean steps, 0}
         self.scaler = None
         self.scale_interval = scale_interval
         if dtype == "fp16":
             self.scaler = torch.tensor([init_scale, 1.0 / init_scale, 0.0, 0.0], dtype=torch.float32,
                                        device=self.device)
+        self.bucket_mb = bucket_mb
+        self.comm_timing = False
+        self._comm_events = []
         self.reducer = reducer
         if self.reducer is None and (world > 1 or reducer_transport is not None):
             from ..parallel.reducer import BucketedReducer
             self.reducer = BucketedReducer(self.arena, self.ex.grad_ready_order(), bucket_mb=bucket_mb,
                                            transport=reducer_transport or "auto")
+        self.reducer_transport = None if self.reducer is None else self.reducer.transport
         if world > 1:
             self._broadcast_params()
         self.use_graph = graph
@@ -94,47 +108,74 @@ class NativeStepper:
             dist.broadcast(self.arena.data, src=0)
         self.ex.refresh_packs(force=True)
 
+    @property
+    def lr(self) -> float:
+        return self._lr
+
+    @lr.setter
+    def lr(self, v: float):
+        """Host value + the device scalar the SGD kernel reads (a captured step sees updates)."""
+        self._lr = float(v)
+        self._lr_dev.fill_(self._lr)
+
     def _step_body(self, img, gt, update: bool = True):
         ex = self.ex
         st = _ext.stream_ptr(self.device)
-        b6, sv = ex.forward_features(img, save=True)
-        ex.workspace(*ex.input_hw(img))
-        sc = self.scaler
-        loss, et, d_b6 = ex.head_train(b6, gt, self.grads, lscale=sc[0:1] if sc is not None else None)
+        with trace_range("cannet/forward"):
+            b6, sv = ex.forward_features(img, save=True)
+            ex.workspace(*ex.input_hw(img))
+            sc = self.scaler
+            # fused head: loss -> flags[1], its non-finite flag -> flags[0] (same kernel, no extra launch)
+            loss, et, d_b6 = ex.head_train(b6, gt, self.grads, lscale=sc[0:1] if sc is not None else None,
+                                           flags=self.flags)
         red = self.reducer
         if red is not None:
             red.begin()
             red.mark_ready([ex.head_w_index, ex.head_b_index])
-        # scalars: [nonfinite flag, loss].  Issued on the weight-gradient side stream, idle at this point,
-        # so the handful of tiny kernels stay off the step's tail; backward_features joins that stream
-        side = ex._side_stream()
-        if side is not None:
-            side.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
-            self.flags[0:1].copy_((~torch.isfinite(loss)).float())
-            self.flags[1:2].copy_(loss)
-        ex.backward_features(sv, d_b6, self.grads, on_grad_ready=(red.mark_ready if red is not None else None),
-                             dscale=sc[1:2] if sc is not None else None)
+        with trace_range("cannet/backward"):
+            ex.backward_features(sv, d_b6, self.grads, on_grad_ready=(red.mark_ready if red is not None else None),
+                                 dscale=sc[1:2] if sc is not None else None)
         del sv
+        timing = self.comm_timing and self.device.type == "cuda"
+        if timing:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
         if red is not None:
-            red.finish()
-            red.allreduce_scalars(self.flags[0:2])
+            with trace_range("cannet/allreduce"):
+                red.finish()
+                red.allreduce_scalars(self.flags[0:2])
+        if timing:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self._comm_events.append((e0, e1))
         if sc is not None:
             # after the all-reduce every rank holds the same gradients -> the same verdict
             self.flags[2:3].zero_()
             self.C.grad_nonfinite(self.arena.grad.data_ptr(), self.arena.numel, self.flags.data_ptr() + 8, st)
         if not update:
             return self.flags[1:2]
-        gscale = 1.0 / self.world
-        self.C.sgd_momentum(self.arena.data.data_ptr(), self.mom.data_ptr(), self.arena.grad.data_ptr(),
-                            self.arena.numel, float(self.lr), float(self.momentum), float(gscale), 0,
-                            self.flags.data_ptr(), st)
-        if sc is not None:
-            self.C.scale_update(self.flags.data_ptr() + 8, sc.data_ptr(), int(self.scale_interval), 2.0, 0.5,
-                                float(2 ** 24), st)
-        ex.refresh_packs(force=True)
-        ex.mark_weights_updated()
+        with trace_range("cannet/sgd"):
+            gscale = 1.0 / self.world
+            self.C.sgd_momentum(self.arena.data.data_ptr(), self.mom.data_ptr(), self.arena.grad.data_ptr(),
+                                self.arena.numel, float(self._lr), float(self.momentum), float(gscale), 0,
+                                self.flags.data_ptr(), self._lr_dev.data_ptr(), st)
+            if sc is not None:
+                self.C.scale_update(self.flags.data_ptr() + 8, sc.data_ptr(), int(self.scale_interval), 2.0, 0.5,
+                                    float(2 ** 24), st)
+            ex.refresh_packs(force=True)
+            ex.mark_weights_updated()
         return self.flags[1:2]
+
+    def exposed_comm_ms(self, reset: bool = True) -> Optional[float]:
+        """Mean device time between 'every gradient written' and 'all-reduce joined back' over the steps run
+        with ``comm_timing`` (the part of the gradient all-reduce NOT hidden behind the backward)."""
+        if not self._comm_events:
+            return None
+        torch.cuda.synchronize(self.device)
+        v = sum(a.elapsed_time(b) for a, b in self._comm_events) / len(self._comm_events)
+        if reset:
+            self._comm_events = []
+        return v
 
     # ------------------------------------------------------------ public
     def step(self, img, gt):
@@ -173,9 +214,13 @@ class NativeStepper:
         return None if self._loss is None else float(self._loss.reshape(-1)[0])
 
     def nonfinite(self) -> bool:
-        """Non-finite loss in the last step (the reference's exit condition).  An fp16 gradient overflow
-        is not one: that step is skipped and the loss scale backed off."""
-        return bool(self.flags[0].item() != 0)
+        """A non-finite loss in ANY step since the last ``reset_nonfinite()`` (the reference's exit condition,
+        utils/train_eval_utils.py:48-50; sticky on the device, so polling every k steps misses none).  An fp16
+        gradient overflow is not one: that step is skipped and the loss scale backed off."""
+        return bool(self.flags[3].item() != 0)
+
+    def reset_nonfinite(self):
+        self.flags[3:4].zero_()
 
     def loss_scale(self) -> float:
         return 1.0 if self.scaler is None else float(self.scaler[0].item())

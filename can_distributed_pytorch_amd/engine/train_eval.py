@@ -11,8 +11,9 @@ Parity: utils/train_eval_utils.py of the reference —
 Native fast path: ``train_one_epoch_native(stepper, ...)`` drives the fused
 NativeStepper (HIP executor + RCCL reducer + fused SGD): no host sync per
 step — the loss is read back only every ``log_every`` steps and the
-non-finite flag (device-side, all-reduced with the loss) is checked at the
-same cadence and at the end of the epoch.
+non-finite flag (device-side, all-reduced with the loss, and latched by the
+SGD kernel so a NaN on a step that is not read is never lost) is checked at
+the same cadence and at the end of the epoch.
 """
 from __future__ import annotations
 
@@ -65,6 +66,7 @@ def train_one_epoch_native(stepper, train_loader, device, epoch, log=None, log_e
     """Fused native step per batch (see engine/native.py).  ``prep`` maps a raw
     loader batch to (img, gt) on the device (GPU preprocessing)."""
     stepper.model.train()
+    stepper.reset_nonfinite()          # the device flag is sticky: any non-finite step of this epoch latches it
     loader = _progress(train_loader, is_main_process())
     total = torch.zeros(1, device=device)
     n = 0

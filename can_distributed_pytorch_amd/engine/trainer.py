@@ -24,7 +24,8 @@ from ..models.cannet import CANNet
 
 
 class TorchStepper:
-    def __init__(self, device, dtype="fp32", world=1, lr=1e-7, momentum=0.95, channels_last=None, model=None):
+    def __init__(self, device, dtype="fp32", world=1, lr=1e-7, momentum=0.95, channels_last=None, model=None,
+                 bucket_mb: float = 25.0):
         self.device = torch.device(device)
         self.model = (model or CANNet(backend="torch")).to(self.device)
         self.model.exec_backend = "torch"
@@ -35,7 +36,8 @@ class TorchStepper:
         self.net = self.model
         if world > 1:
             dev_ids = [self.device.index] if self.device.type == "cuda" else None
-            self.net = torch.nn.parallel.DistributedDataParallel(self.model, device_ids=dev_ids)
+            self.net = torch.nn.parallel.DistributedDataParallel(self.model, device_ids=dev_ids,
+                                                                 bucket_cap_mb=bucket_mb)
         self.opt = torch.optim.SGD([p for p in self.model.parameters() if p.requires_grad],
                                    lr=lr * world, momentum=momentum, weight_decay=0)
         self.crit = torch.nn.MSELoss(reduction="sum")
@@ -69,9 +71,11 @@ class TorchStepper:
 
 
 def build_trainer(impl="hip", dtype="bf16", device="cuda", world=1, lr=1e-7, batch=8,
-                  height=768, width=1024, graph=True, model=None):
+                  height=768, width=1024, graph=True, model=None, bucket_mb: float = 25.0,
+                  reducer_transport: Optional[str] = None):
     if impl == "torch":
-        return TorchStepper(device, dtype=dtype, world=world, lr=lr, model=model)
+        return TorchStepper(device, dtype=dtype, world=world, lr=lr, model=model, bucket_mb=bucket_mb)
     from .native import NativeStepper
     return NativeStepper(device, dtype=dtype, world=world, lr=lr, batch=batch, height=height,
-                         width=width, graph=graph, model=model)
+                         width=width, graph=graph, model=model, bucket_mb=bucket_mb,
+                         reducer_transport=reducer_transport)

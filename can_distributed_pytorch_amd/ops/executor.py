@@ -277,11 +277,9 @@ class CANNetExecutor:
         rowacc = torch.empty(n, h, 12, c, dtype=torch.float32, device=fv.device)
         ave = torch.empty(n, 50, c, dtype=torch.float32, device=fv.device)
         self.C.ctx_reduce(0, fv.data_ptr(), 0, 0, rowacc.data_ptr(), ave.data_ptr(), n, h, w, c, self.dt, st)
+        # conv{S}_1 on the pooled grids: the four scales' fp32 GEMMs in one launch
         table = torch.empty_like(ave)
-        for sc in CONTEXT_SCALES:
-            o, k = CELL_OFF[sc], sc * sc
-            w1 = self.ctx1[sc].weight.detach().view(c, c)
-            torch.matmul(ave[:, o:o + k], w1.t(), out=table[:, o:o + k])
+        self.C.ctx_gemm(0, ave.data_ptr(), 0, self._ctx1_ptrs(), table.data_ptr(), [], n, c, 0.0, 1.0, 0, st)
         cs = torch.empty(4, n, h, w, c, dtype=self.act, device=fv.device)
         self.C.ctx_expand(fv.data_ptr(), table.data_ptr(), cs.data_ptr(), n, h, w, c, self.dt, st)
         wts = torch.empty(4, n, h, w, c, dtype=self.act, device=fv.device)
@@ -292,6 +290,13 @@ class CANNetExecutor:
         self.C.ctx_fuse(fv.data_ptr(), wts.data_ptr(), table.data_ptr(), cat.data_ptr(), n, h, w, c, self.dt, st)
         saved = dict(ave=ave, table=table, cs=cs, wts=wts, rowacc=rowacc) if save else None
         return cat, saved
+
+    def _ctx1_ptrs(self):
+        ws = [self.ctx1[sc].weight for sc in CONTEXT_SCALES]
+        for w_ in ws:
+            if not (w_.is_contiguous() and w_.dtype == torch.float32):
+                raise ValueError("conv{S}_1 weights must be contiguous fp32")
+        return [w_.data_ptr() for w_ in ws]
 
     def head_forward(self, b6):
         n, h, w, _ = b6.shape
@@ -436,25 +441,16 @@ class CANNetExecutor:
         ave = ctx["ave"]
 
         def ctx1_wgrad():
-            for sc in CONTEXT_SCALES:
-                o, k = CELL_OFF[sc], sc * sc
-                gA = dA[:, o:o + k].reshape(-1, c)
-                g = grads[self.ctx1_index[sc]].view(c, c)
-                gw = gA.t() @ ave[:, o:o + k].reshape(-1, c)
-                if scale != 1.0:
-                    gw = gw * scale
-                if dscale is not None:
-                    gw = gw * dscale
-                if beta:
-                    g.add_(gw)
-                else:
-                    g.copy_(gw)
+            # dW1_S = dA_S^T @ ave_S for the four scales, one launch (on the weight-gradient stream)
+            gws = [grads[self.ctx1_index[sc]] for sc in CONTEXT_SCALES]
+            for g in gws:
+                if not (g.is_contiguous() and g.dtype == torch.float32):
+                    raise ValueError("conv{S}_1 gradient buffers must be contiguous fp32")
+            self.C.ctx_gemm(2, dA.data_ptr(), ave.data_ptr(), [], 0, [g.data_ptr() for g in gws], n, c, float(beta),
+                            float(scale), dscale.data_ptr() if dscale is not None else 0, self._stream())
             ready([self.ctx1_index[sc] for sc in CONTEXT_SCALES])
-        self._on_side(side, ctx1_wgrad, hold, dA)
-        for sc in CONTEXT_SCALES:
-            o, k = CELL_OFF[sc], sc * sc
-            w1 = self.ctx1[sc].weight.detach().view(c, c)
-            torch.matmul(dA[:, o:o + k], w1, out=dave[:, o:o + k])
+        self._on_side(side, ctx1_wgrad, hold, dA, ave)
+        self.C.ctx_gemm(1, dA.data_ptr(), 0, self._ctx1_ptrs(), dave.data_ptr(), [], n, c, 0.0, 1.0, 0, st)
         dfv = torch.empty(n, h, w, c, dtype=self.act, device=fv.device)
         self.C.ctx_bwd_final(dcat.data_ptr(), dc.data_ptr(), dave.data_ptr(), fv.data_ptr(), dfv.data_ptr(), n, h, w,
                              c, self.dt, st)
@@ -474,9 +470,11 @@ class CANNetExecutor:
 
     # ----------------------------------------------------------- training head
     def head_train(self, b6, gt, grads, gscale: float = 1.0, beta: float = 0.0,
-                   lscale: Optional[torch.Tensor] = None):
+                   lscale: Optional[torch.Tensor] = None, flags: Optional[torch.Tensor] = None):
         """Fused: et, MSE(sum) loss, d(et), d(b6 pre-act) (ReLU-masked), head grads. Returns (loss, et, d_b6).
-        lscale: optional fp32 device scalar (loss scale) applied to d_b6 only; head grads stay unscaled."""
+        lscale: optional fp32 device scalar (loss scale) applied to d_b6 only; head grads stay unscaled.
+        flags: optional fp32 device vector; the loss is written to flags[1] and its non-finite flag
+        (1.0 / 0.0) to flags[0] by the same reduction kernel (the returned loss is then flags[1:2])."""
         n, h, w, c = b6.shape
         if tuple(gt.shape) != (n, 1, h, w):
             raise ValueError(f"gt shape {tuple(gt.shape)} != {(n, 1, h, w)}")
@@ -486,11 +484,16 @@ class CANNetExecutor:
         d_b6 = torch.empty_like(b6)
         nblk = max(1, min(1024, (P * 8 + 255) // 256))
         part = torch.empty(nblk, 66, dtype=torch.float32, device=b6.device)
-        loss = torch.empty(1, dtype=torch.float32, device=b6.device)
+        if flags is not None:
+            if not (flags.dtype == torch.float32 and flags.is_contiguous() and flags.numel() >= 2):
+                raise ValueError("flags must be a contiguous fp32 vector of >= 2 elements")
+            loss, nf = flags[1:2], flags.data_ptr()
+        else:
+            loss, nf = torch.empty(1, dtype=torch.float32, device=b6.device), 0
         self.C.head_train(b6.data_ptr(), self.head.weight.detach().data_ptr(), self.head.bias.detach().data_ptr(),
                           gt.data_ptr(), et.data_ptr(), d_b6.data_ptr(), part.data_ptr(), nblk,
                           grads[self.head_w_index].data_ptr(), grads[self.head_b_index].data_ptr(), loss.data_ptr(),
-                          P, float(gscale), float(beta), lscale.data_ptr() if lscale is not None else 0, self.dt,
+                          P, float(gscale), float(beta), lscale.data_ptr() if lscale is not None else 0, nf, self.dt,
                           self._stream())
         return loss, et, d_b6
 

@@ -10,8 +10,9 @@ Differences by design:
   * Q5: the SLURM branch reads SLURM_NTASKS / SLURM_LOCALID.
   * One process per GPU; backend "nccl" is RCCL on ROCm (xGMI intra-node).
     On CPU (tests, fake clusters) the backend is gloo.
-  * The TCPStore created by the rendezvous is kept and re-used by the native
-    RCCL communicator (ncclUniqueId exchange) in parallel/comm.py.
+  * The native RCCL communicator (csrc/rccl_reducer.cpp) gets its
+    ncclUniqueId through this process group (parallel/reducer.py:
+    make_rccl_comm, one broadcast_object_list).
 """
 from __future__ import annotations
 

@@ -3,9 +3,12 @@
 The RCCL communicator refuses two ranks on one device, so the multi-rank
 logic of the native step (init broadcast, gradient-ready bucket launches,
 scalar reduction, lr x world with 1/world averaging folded into the fused
-SGD) is exercised here through the reducer's torch/gloo transport; the RCCL
-transport itself is covered at world 1 (test_gpu_executor.py) and runs at
-world 8 in the driver's scaling bench.
+SGD) is exercised here through the reducer's torch/gloo transport.  The RCCL
+transport's own GPU coverage is world 1 (test_gpu_executor.py); its
+multi-rank scheduling logic (the C++ BucketSchedule it shares with the CPU
+fake-cluster transport) is tested with 2-4 fake ranks in
+tests/test_reducer_native.py.  Multi-GPU RCCL execution happens only on an
+8-GPU node (the driver's scaling bench), which this suite cannot reach.
 
 Equivalence checked: 2-rank DP over batches b0, b1 with the reference's lr
 scaling (train.py:25) == one process over cat(b0, b1) at the base lr, since
