@@ -479,11 +479,53 @@ struct CtxGemmArgs {
 
 __device__ __forceinline__ int ctx_cell_row(int r, int k2, int off) { return (r / k2) * 50 + off + (r % k2); }
 
+// One K tile (32 deep) of X (32 x 32) and Y (32 x 64) in registers, 16-B loads: every load of the tile is
+// issued before any is consumed (the first version stored each element to LDS right after its load, which
+// serialised ~12 memory latencies per K step).
+template <int MODE>
+struct CtxTile {
+  float4 x, y0, y1;
+};
+
+template <int MODE>
+__device__ __forceinline__ CtxTile<MODE> ctx_load(const CtxGemmArgs& a, const float* W, int m0, int n0, int k0,
+                                                  int M, int K, int k2, int off, int tid) {
+  const int C = a.C;
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  CtxTile<MODE> t;
+  if (MODE == 2) {
+    // X(m,k) = dA[row(k)][m]: m contiguous; tile element (k = tid/8, m4 = tid%8)
+    const int k = k0 + (tid >> 3), m = m0 + (tid & 7) * 4;
+    t.x = (k < K) ? *reinterpret_cast<const float4*>(a.x + (size_t)ctx_cell_row(k, k2, off) * C + m) : z;
+  } else {
+    // X(m,k) = cells[row(m)][k]: k contiguous; (m = tid/8, k4 = tid%8)
+    const int m = m0 + (tid >> 3), k = k0 + (tid & 7) * 4;
+    t.x = (m < M) ? *reinterpret_cast<const float4*>(a.x + (size_t)ctx_cell_row(m, k2, off) * C + k) : z;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int e = tid + 256 * i;
+    float4 v;
+    if (MODE == 0) {
+      // Y(k,n) = W[n][k]: k contiguous; (n = e/8, k4 = e%8)
+      const int n = n0 + (e >> 3), k = k0 + (e & 7) * 4;
+      v = *reinterpret_cast<const float4*>(W + (size_t)n * C + k);
+    } else {
+      // Y(k,n) = W[k][n] (MODE 1) / ave[row(k)][n] (MODE 2): n contiguous; (k = e/16, n4 = e%16)
+      const int k = k0 + (e >> 4), n = n0 + (e & 15) * 4;
+      if (MODE == 1) v = *reinterpret_cast<const float4*>(W + (size_t)k * C + n);
+      else v = (k < K) ? *reinterpret_cast<const float4*>(a.y + (size_t)ctx_cell_row(k, k2, off) * C + n) : z;
+    }
+    if (i == 0) t.y0 = v; else t.y1 = v;
+  }
+  return t;
+}
+
 template <int MODE>
 __global__ void __launch_bounds__(256) ctx_gemm_kernel(CtxGemmArgs a) {
   constexpr int TM = 32, TN = 64, TK = 32;
-  __shared__ float Xs[TK][TM + 1];
-  __shared__ float Ys[TK][TN + 4];
+  __shared__ __attribute__((aligned(16))) float Xs[TK][TM + 4];
+  __shared__ __attribute__((aligned(16))) float Ys[TK][TN + 4];
   const int si = blockIdx.z;
   const int S = (si == 0) ? 1 : (si == 1) ? 2 : (si == 2) ? 3 : 6;
   const int off = (si == 0) ? 0 : (si == 1) ? 1 : (si == 2) ? 5 : 14;
@@ -494,33 +536,28 @@ __global__ void __launch_bounds__(256) ctx_gemm_kernel(CtxGemmArgs a) {
   const float* W = a.w[si];
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
   float acc[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  CtxTile<MODE> cur = ctx_load<MODE>(a, W, m0, n0, 0, M, K, k2, off, tid);
   for (int k0 = 0; k0 < K; k0 += TK) {
-    for (int e = tid; e < TM * TK; e += 256) {
-      int mm, kk;
-      if (MODE == 2) { mm = e % TM; kk = e / TM; }   // dA[row(k)][m]: m contiguous
-      else { kk = e % TK; mm = e / TK; }             // cells[row(m)][k]: k contiguous
-      const int m = m0 + mm, k = k0 + kk;
-      float v = 0.f;
-      if (m < M && k < K) {
-        if (MODE == 2) v = a.x[(size_t)ctx_cell_row(k, k2, off) * C + m];
-        else v = a.x[(size_t)ctx_cell_row(m, k2, off) * C + k];
-      }
-      Xs[kk][mm] = v;
+    // registers -> LDS
+    if (MODE == 2) {
+      *reinterpret_cast<float4*>(&Xs[tid >> 3][(tid & 7) * 4]) = cur.x;
+    } else {
+      const int mm = tid >> 3, kk = (tid & 7) * 4;
+      Xs[kk][mm] = cur.x.x; Xs[kk + 1][mm] = cur.x.y; Xs[kk + 2][mm] = cur.x.z; Xs[kk + 3][mm] = cur.x.w;
     }
-    for (int e = tid; e < TK * TN; e += 256) {
-      int kk, nn;
-      if (MODE == 0) { kk = e % TK; nn = e / TK; }   // W[n][k]: k contiguous
-      else { nn = e % TN; kk = e / TN; }             // W[k][n] / ave[row(k)][n]: n contiguous
-      const int k = k0 + kk, n = n0 + nn;
-      float v = 0.f;
-      if (k < K && n < C) {
-        if (MODE == 0) v = W[(size_t)n * C + k];
-        else if (MODE == 1) v = W[(size_t)k * C + n];
-        else v = a.y[(size_t)ctx_cell_row(k, k2, off) * C + n];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + 256 * i;
+      const float4 v = i ? cur.y1 : cur.y0;
+      if (MODE == 0) {
+        const int nn = e >> 3, kk = (e & 7) * 4;
+        Ys[kk][nn] = v.x; Ys[kk + 1][nn] = v.y; Ys[kk + 2][nn] = v.z; Ys[kk + 3][nn] = v.w;
+      } else {
+        *reinterpret_cast<float4*>(&Ys[e >> 4][(e & 15) * 4]) = v;
       }
-      Ys[kk][nn] = v;
     }
     __syncthreads();
+    if (k0 + TK < K) cur = ctx_load<MODE>(a, W, m0, n0, k0 + TK, M, K, k2, off, tid);   // next tile in flight
 #pragma unroll 8
     for (int kk = 0; kk < TK; ++kk) {
       const float x0 = Xs[kk][ty * 2], x1 = Xs[kk][ty * 2 + 1];
@@ -630,7 +667,7 @@ extern "C" int can_ctx_bwd_final(const void* dcat, const void* dc, const float* 
 extern "C" int can_ctx_gemm(int mode, const float* x, const float* y, const float* const* w, float* out,
                             float* const* gw, int N, int C, float beta, float scale, const float* dscale,
                             void* stream) {
-  if (C % 64 != 0 || N < 1) return -2;
+  if (C % 64 != 0 || N < 1) return -2;   // 16-B rows, 64-column tiles
   CtxGemmArgs a{};
   a.x = x; a.y = y; a.out = out; a.N = N; a.C = C; a.beta = beta; a.scale = scale; a.dscale = dscale;
   for (int i = 0; i < 4; ++i) {
