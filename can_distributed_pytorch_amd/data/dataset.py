@@ -7,14 +7,19 @@ of d, a random horizontal flip of BOTH in phase 'train', and the ground
 truth loaded from ``gt_dmap_root/<name>.npy`` (``.jpg`` -> ``.npy``).
 
 Differences: gt_downsample <= 1 works (Q8), integer
-images only are /255 (Q14), decoding uses PIL (cv2 is not a dependency),
-the flip RNG is seedable.  ``SyntheticCrowdDataset`` provides the same item
-contract without files (benchmarks, tests, smoke runs).
+images only are /255 (Q14), decoding uses PIL (cv2 is not a dependency).
+The random flip (model/CrowdDataset.py:48-50, Python ``random`` there) is a
+pure function of (seed, epoch, index) — a counter-based hash, no RNG state:
+DataLoader workers cannot replay one another's stream (a ``random.Random``
+pickled into every worker would), and a resumed run draws exactly the flips
+of an uninterrupted one.  The epoch comes from ``set_epoch`` or, with
+worker processes, travels with the index (``EpochTaggedSampler``).
+``SyntheticCrowdDataset`` provides the same item contract without files
+(benchmarks, tests, smoke runs).
 """
 from __future__ import annotations
 
 import os
-import random
 from typing import Optional
 
 import numpy as np
@@ -24,6 +29,43 @@ from torch.utils.data import Dataset
 from .transforms import prepare_pair
 
 IMG_EXT = (".jpg", ".jpeg", ".png", ".bmp", ".tif", ".tiff")
+_M64 = (1 << 64) - 1
+
+
+def _splitmix64(x: int) -> int:
+    x = (x + 0x9E3779B97F4A7C15) & _M64
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & _M64
+    return x ^ (x >> 31)
+
+
+def flip_draw(seed: int, epoch: int, index: int) -> bool:
+    """The p=0.5 horizontal flip of sample ``index`` in ``epoch`` (stateless, worker-independent)."""
+    return bool(_splitmix64(_splitmix64(_splitmix64(seed & _M64) ^ (epoch & _M64)) ^ (index & _M64)) >> 63)
+
+
+class EpochTaggedSampler:
+    """Wraps a sampler (e.g. DistributedSampler) so that every index carries the sampler's epoch:
+    yields (index, epoch) pairs, which ``CrowdDataset.__getitem__`` accepts.  Needed because persistent
+    DataLoader workers hold their own copy of the dataset (``dataset.set_epoch`` in the main process would
+    not reach them)."""
+
+    def __init__(self, sampler):
+        self.sampler = sampler
+
+    def set_epoch(self, epoch: int):
+        self.sampler.set_epoch(epoch)
+
+    def __iter__(self):
+        ep = int(getattr(self.sampler, "epoch", 0))
+        for i in self.sampler:
+            yield (int(i), ep)
+
+    def __len__(self):
+        return len(self.sampler)
+
+    def __getattr__(self, name):          # total_size, num_replicas, ... of the wrapped sampler
+        return getattr(self.sampler, name)
 
 
 def imread(path: str) -> np.ndarray:
@@ -44,7 +86,8 @@ class CrowdDataset(Dataset):
         self.img_names = sorted(f for f in os.listdir(img_root)
                                 if os.path.isfile(os.path.join(img_root, f)) and f.lower().endswith(IMG_EXT))
         self.n_samples = len(self.img_names)
-        self._rng = random.Random(seed)
+        self.seed = 0 if seed is None else int(seed)
+        self.epoch = 0
         # raw=True: return (uint8 image, full-res density, flip) and let the GPU
         # preprocess it (ops/preprocess.py) instead of resizing on the CPU
         self.raw = raw
@@ -52,17 +95,23 @@ class CrowdDataset(Dataset):
     def __len__(self):
         return self.n_samples
 
+    def set_epoch(self, epoch: int):
+        self.epoch = int(epoch)
+
     def gt_path(self, name: str) -> str:
         stem = os.path.splitext(name)[0]
         return os.path.join(self.gt_dmap_root, stem + ".npy")
 
     def __getitem__(self, index):
+        epoch = self.epoch
+        if isinstance(index, (tuple, list)):
+            index, epoch = int(index[0]), int(index[1])
         if not 0 <= index < len(self):
             raise IndexError("index range error")
         name = self.img_names[index]
         img = imread(os.path.join(self.img_root, name))
         dmap = np.load(self.gt_path(name))                       # allow_pickle=False (default)
-        flip = self.phase == "train" and self._rng.randint(0, 1) == 1
+        flip = self.phase == "train" and flip_draw(self.seed, epoch, index)
         if self.raw:
             if img.dtype != np.uint8:
                 img = np.clip(np.asarray(img, dtype=np.float64) * (255.0 if img.dtype.kind == "f" else 1.0),
@@ -91,5 +140,7 @@ class SyntheticCrowdDataset(Dataset):
         return self.n
 
     def __getitem__(self, index):
+        if isinstance(index, (tuple, list)):
+            index = int(index[0])
         img, gt = self._make(1, self.h, self.w, seed=self.seed * 100003 + index, heads=self.heads)
         return img[0], gt[0]

@@ -75,7 +75,7 @@ def gaussian_filter_density(img_or_shape, points: Union[np.ndarray, Sequence]) -
     return density.astype(np.float32)
 
 
-def density_map_gpu(points, h: int, w: int, device="cuda", max_radius: int = 511) -> torch.Tensor:
+def density_map_gpu(points, h: int, w: int, device="cuda", max_radius: int = 0) -> torch.Tensor:
     """GPU density map [h, w] fp32 for points [[x, y], ...]."""
     from ..ops import _ext
     C = _ext.require()

@@ -210,6 +210,22 @@ class NativeStepper:
             self._static_loss = self._step_body(self.static_img, self.static_gt)
         torch.cuda.synchronize(self.device)
 
+    def resume_state(self) -> dict:
+        """Device state a resumed run needs besides weights and momentum (checkpoint.save_train_state)."""
+        st = {"lr": self._lr, "steps": self.steps}
+        if self.scaler is not None:
+            st["scaler"] = self.scaler
+        return st
+
+    def load_resume_state(self, st: Optional[dict]):
+        if not st:
+            return
+        self.lr = float(st.get("lr", self._lr))
+        self.steps = int(st.get("steps", self.steps))
+        if self.scaler is not None and st.get("scaler") is not None:
+            self.scaler.copy_(st["scaler"].to(self.scaler.device))
+        self.ex.refresh_packs(force=True)
+
     def last_loss(self) -> Optional[float]:
         return None if self._loss is None else float(self._loss.reshape(-1)[0])
 

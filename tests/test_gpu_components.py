@@ -154,6 +154,21 @@ def test_density_gpu_matches_cpu():
     assert abs(got.sum() - ref.sum()) < 1e-2
 
 
+@pytest.mark.parametrize("npts", [1, 3])
+def test_density_gpu_large_radius_matches_cpu(npts):
+    """Footprints wider than 1023 px: the single-head case sigma = (H+W)/8 = 224 at 768x1024 (R = 896) and
+    three heads far apart (kNN sigmas ~ 0.1 * (d1+d2) >> 128).  Exact radius, mass outside the image dropped
+    after normalising, as scipy's gaussian_filter on a delta (radius was clamped at 511)."""
+    import numpy as np
+    from can_distributed_pytorch_amd.data.density import density_map_gpu, gaussian_filter_density
+    h, w = 768, 1024
+    pts = np.array([[500.3, 380.7], [20.0, 30.0], [1000.0, 750.0]], dtype=np.float32)[:npts]
+    ref = gaussian_filter_density((h, w), pts)
+    got = density_map_gpu(pts, h, w).cpu().numpy()
+    assert np.abs(got - ref).max() < 1e-7 + 1e-4 * np.abs(ref).max()
+    assert abs(got.sum() - ref.sum()) < 1e-4 * npts
+
+
 def test_no_uninitialized_reads_poisoned_allocator():
     """Regression: fill the caching allocator with NaN bit patterns before every
     buffer the executor allocates; outputs must not change (a NaN read from an

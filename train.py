@@ -99,12 +99,14 @@ def make_loaders(args, world, rank, raw=False):
     else:
         r = args.data_root
         train_ds = CrowdDataset(os.path.join(r, "train_data", "images"), os.path.join(r, "train_data", "ground_truth"),
-                                gt_downsample=8, phase="train", seed=args.seed + rank, raw=raw)
+                                gt_downsample=8, phase="train", seed=args.seed, raw=raw)
         test_ds = CrowdDataset(os.path.join(r, "test_data", "images"), os.path.join(r, "test_data", "ground_truth"),
                                gt_downsample=8, phase="test", raw=raw)
+    from can_distributed_pytorch_amd.data.dataset import EpochTaggedSampler
     train_sampler = DistributedSampler(train_ds, num_replicas=world, rank=rank, shuffle=True, seed=args.seed)
     test_sampler = DistributedSampler(test_ds, num_replicas=world, rank=rank, shuffle=True, seed=args.seed)
-    bs = BatchSampler(train_sampler, args.batch_size, drop_last=False)
+    # indices carry the epoch into (persistent) workers: the flip is a function of (seed, epoch, index)
+    bs = BatchSampler(EpochTaggedSampler(train_sampler), args.batch_size, drop_last=False)
     pin = torch.cuda.is_available()
     train_loader = DataLoader(train_ds, batch_sampler=bs, num_workers=args.num_workers, pin_memory=pin,
                               persistent_workers=args.num_workers > 0, collate_fn=collate)
@@ -171,10 +173,11 @@ def main(args):
 
     start_epoch, min_mae, min_epoch = 0, float("inf"), 0
     if args.resume and os.path.exists(args.resume):
-        start_epoch, min_mae = load_train_state(args.resume, stepper.model, momentum)
-        start_epoch += 1
+        rs = load_train_state(args.resume, stepper.model, momentum,
+                              optimizer=None if args.impl == "hip" else stepper.opt)
+        start_epoch, min_mae, min_epoch = rs["epoch"] + 1, rs["min_mae"], rs["min_epoch"]
         if args.impl == "hip":
-            stepper.ex.refresh_packs(force=True)
+            stepper.load_resume_state(rs["stepper"])
 
     from can_distributed_pytorch_amd.engine.train_eval import train_one_epoch_native, evaluate, train_one_epoch
     import math
@@ -211,7 +214,8 @@ def main(args):
                 min_mae, min_epoch = mean_mae, epoch
                 save_checkpoint(stepper.model, os.path.join(args.checkpoint_dir, f"epoch_{epoch}.pth"))
             save_train_state(os.path.join(args.checkpoint_dir, "last_state.pth"), stepper.model, momentum, epoch,
-                             min_mae)
+                             min_mae, optimizer=None if args.impl == "hip" else stepper.opt, min_epoch=min_epoch,
+                             stepper_state=stepper.resume_state() if args.impl == "hip" else None)
             lr_now = stepper.lr if args.impl == "hip" else stepper.opt.param_groups[0]["lr"]
             ips = len(train_loader) * args.batch_size * world / max(t_train, 1e-9)
             print(f"[epoch {epoch}] loss: {mean_loss:.4f} mae: {mean_mae:.3f}, min_mae: {min_mae:.3f}, "
