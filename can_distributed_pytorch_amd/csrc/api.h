@@ -11,7 +11,7 @@ int can_conv_igemm(const void* x, const void* w, const float* bias, const void* 
                    int Cin, int Cout, int ksize, int dil, int epi, int first, int tile_cfg, int dt, void* stream);
 
 int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, int target_blocks, int* S_out, int* mslice_out,
-                   int* cfg_out);
+                   int* cfg_out, int dil);
 int can_conv_wgrad(const void* dy, const void* x, float* ws, float* wsb, float* dw, float* db, int N, int H, int W,
                    int Cin, int Cout, int ksize, int dil, int first, int S, int mslice, int cfg, float beta,
                    float scale, const float* dscale, int dt, void* stream);
@@ -21,8 +21,9 @@ int can_conv_wgrad_1x1_batched(const void* dy, const void* x, float* ws, float* 
                                float scale, const float* dscale, int dt, void* stream);
 
 // conv + bias + ReLU with the 2x2/s2 max-pool fused into the epilogue (y full resolution, yp pooled)
-int can_conv_pool_fwd(const void* x, const void* w, const float* bias, void* y, void* yp, int N, int H, int W,
-                      int Cin, int Cout, int ksize, int dil, int tile_cfg, int dt, void* stream);
+// codes: max-pool codes uint32 [N][H/2][W/2][Cout/8] (optional), y optional (nullptr: not written)
+int can_conv_pool_fwd(const void* x, const void* w, const float* bias, void* y, void* yp, void* codes, int N, int H,
+                      int W, int Cin, int Cout, int ksize, int dil, int tile_cfg, int dt, void* stream);
 int can_conv_pool_tp(int Cin, int Cout, int ksize, int tile_cfg);
 
 // conv1_2 with conv1_1's output recomputed from the NHWC4 image (never stored)
@@ -33,7 +34,9 @@ int can_conv_wgrad_f1(const void* dy, const void* img, const void* w1, const flo
                       int dt, void* stream);
 
 // elementwise.hip
-int can_maxpool_fwd(const void* x, void* y, int N, int H, int W, int C, int dt, void* stream);
+int can_maxpool_fwd(const void* x, void* y, void* codes, int N, int H, int W, int C, int dt, void* stream);
+int can_maxpool_bwd_codes(const void* codes, const void* dy, void* dx, int N, int H, int W, int C, int dt,
+                          void* stream);
 int can_maxpool_bwd_relu(const void* x, const void* dy, void* dx, int N, int H, int W, int C, int dt, void* stream);
 int can_head_fwd(const void* y, const float* w, const float* b, float* et, int P, int dt, void* stream);
 int can_head_train(const void* y, const float* w, const float* b, const float* gt, float* et, void* dy, float* part,

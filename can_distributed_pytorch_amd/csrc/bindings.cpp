@@ -48,11 +48,12 @@ PYBIND11_MODULE(CAN_MODULE_NAME, m) {
           "conv_igemm");
   });
 
-  m.def("wgrad_plan", [](int M, int Cin, int Cout, int ksize, int first, int target_blocks) {
+  m.def("wgrad_plan", [](int M, int Cin, int Cout, int ksize, int first, int target_blocks, int dil) {
     int S = 0, ms = 0, cfg = 0;
-    check(can_wgrad_plan(M, Cin, Cout, ksize, first, target_blocks, &S, &ms, &cfg), "wgrad_plan");
+    check(can_wgrad_plan(M, Cin, Cout, ksize, first, target_blocks, &S, &ms, &cfg, dil), "wgrad_plan");
     return py::make_tuple(S, ms, cfg);
-  });
+  }, py::arg("M"), py::arg("Cin"), py::arg("Cout"), py::arg("ksize"), py::arg("first"), py::arg("target_blocks"),
+     py::arg("dil") = 1);
   m.def("conv_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t ws, uintptr_t wsb, uintptr_t dw, uintptr_t db, int N,
                          int H, int W, int Cin, int Cout, int ksize, int dil, int first, int S, int mslice, int cfg,
                          float beta, float scale, uintptr_t dscale, int dt, uintptr_t stream) {
@@ -69,10 +70,11 @@ PYBIND11_MODULE(CAN_MODULE_NAME, m) {
           "conv_wgrad_1x1_batched");
   });
 
-  m.def("conv_pool_fwd", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, uintptr_t yp, int N, int H, int W,
-                            int Cin, int Cout, int ksize, int dil, int tile_cfg, int dt, uintptr_t stream) {
-    check(can_conv_pool_fwd(P(x), P(w), (const float*)bias, P(y), P(yp), N, H, W, Cin, Cout, ksize, dil, tile_cfg,
-                            dt, P(stream)),
+  m.def("conv_pool_fwd", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, uintptr_t yp, uintptr_t codes,
+                            int N, int H, int W, int Cin, int Cout, int ksize, int dil, int tile_cfg, int dt,
+                            uintptr_t stream) {
+    check(can_conv_pool_fwd(P(x), P(w), (const float*)bias, P(y), P(yp), P(codes), N, H, W, Cin, Cout, ksize, dil,
+                            tile_cfg, dt, P(stream)),
           "conv_pool_fwd");
   });
   m.def("conv_pool_tp", &can_conv_pool_tp);
@@ -92,8 +94,14 @@ PYBIND11_MODULE(CAN_MODULE_NAME, m) {
   });
 
   // ---- elementwise
-  m.def("maxpool_fwd", [](uintptr_t x, uintptr_t y, int N, int H, int W, int C, int dt, uintptr_t st) {
-    check(can_maxpool_fwd(P(x), P(y), N, H, W, C, dt, P(st)), "maxpool_fwd");
+  m.def("maxpool_fwd", [](uintptr_t x, uintptr_t y, int N, int H, int W, int C, int dt, uintptr_t st,
+                          uintptr_t codes) {
+    check(can_maxpool_fwd(P(x), P(y), P(codes), N, H, W, C, dt, P(st)), "maxpool_fwd");
+  }, py::arg("x"), py::arg("y"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("dt"),
+     py::arg("st"), py::arg("codes") = 0);
+  m.def("maxpool_bwd_codes", [](uintptr_t codes, uintptr_t dy, uintptr_t dx, int N, int H, int W, int C, int dt,
+                                uintptr_t st) {
+    check(can_maxpool_bwd_codes(P(codes), P(dy), P(dx), N, H, W, C, dt, P(st)), "maxpool_bwd_codes");
   });
   m.def("maxpool_bwd_relu", [](uintptr_t x, uintptr_t dy, uintptr_t dx, int N, int H, int W, int C, int dt,
                                uintptr_t st) {

@@ -44,9 +44,14 @@ struct ConvArgs {
   int N, H, W, Cin, Cout, ksize, dil, M;
 };
 
+// Max-pool codes: the forward pool epilogues record, per pooled pixel and channel, a 4-bit one-hot of the
+// FIRST max of its 2x2 window (ATen scan order (0,0),(0,1),(1,0),(1,1) = bit 0..3), or 0 when that max is
+// not > 0 (the ReLU mask of the pool input).  uint32 codes[N][H/2][W/2][C/8], channel c in word c/8,
+// nibble c%8.  That is everything the backward needs, so the full-resolution pre-pool activation
+// (805 MB for conv1_2 at batch 8 x 768 x 1024) is never written nor re-read.
 // EPI_POOLBWD (LDS-DMA kernels only): the GEMM output is the gradient of a 2x2/s2 max-pool output; the
-// epilogue scatters it straight into the pool INPUT gradient (a.mask = pool input, a.y = its gradient,
-// both [N][2H][2W][Cout]): first max of each window wins (ATen order), times the ReLU mask (max > 0).
+// epilogue scatters it straight into the pool INPUT gradient through the codes (a.pcodes, pooled
+// resolution) into a.y [N][2H][2W][Cout].
 // EPI_POOLFWD (LDS-DMA v2 kernel only, H even, W % (TP/2) == 0): bias + ReLU like EPI_BIAS_RELU, and
 // the 2x2/s2 max-pool of the result is written to a.yp [N][H/2][W/2][Cout] in the same epilogue.  A pixel
 // tile is then 2 image rows x TP/2 columns with the rows interleaved inside each 16-pixel MFMA fragment
@@ -308,6 +313,8 @@ struct ConvArgs2 {
   int H, W, Cin, Cout, ksize, dil, M;
   FastDiv fdW, fdH;
   bf16_t* yp = nullptr;   // EPI_POOLFWD: pooled output [N][H/2][W/2][Cout]
+  uint32_t* codes = nullptr;         // EPI_POOLFWD: max-pool codes (optional); a.y optional too
+  const uint32_t* pcodes = nullptr;  // EPI_POOLBWD: max-pool codes of the pool this gradient goes through
 };
 
 // pixel m of row r of pixel tile pt; EPI_POOLFWD tiles are 2 rows x TP/2 columns, rows interleaved per
@@ -348,7 +355,8 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[j * 4 + r] = acc[j][i][r];
     if constexpr (EPI == EPI_POOLBWD) {
-      // pooled pixel m = (n, ph, pw) -> window rows 2ph, 2ph+1, columns 2pw, 2pw+1 of the full map
+      // pooled pixel m = (n, ph, pw) -> window rows 2ph, 2ph+1, columns 2pw, 2pw+1 of the full map; the
+      // window position w (ATen order) gets the gradient iff bit w of the channel's code is set
       const uint32_t q = fdiv((uint32_t)m, a.fdW);
       const int pw = m - (int)q * a.W;
       const uint32_t n = fdiv(q, a.fdH);
@@ -356,23 +364,13 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
       const size_t W2 = 2 * (size_t)a.W;
       const size_t b0 = (((size_t)n * 2 * a.H + 2 * ph) * W2 + 2 * pw) * a.Cout + chb;
       const size_t off[4] = {b0, b0 + a.Cout, b0 + W2 * a.Cout, b0 + W2 * a.Cout + a.Cout};
-      float x[4][16];
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        unpack8h<DT>(*reinterpret_cast<const uint4*>(a.mask + off[w]), x[w]);
-        unpack8h<DT>(*reinterpret_cast<const uint4*>(a.mask + off[w] + 8), x[w] + 8);
-      }
+      const uint2 cw = *reinterpret_cast<const uint2*>(a.pcodes + (size_t)m * (a.Cout >> 3) + (chb >> 3));
       float o[4][16];
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
-        int arg = 0;
-        float mv = x[0][c];
+        const unsigned nib = ((c < 8 ? cw.x : cw.y) >> (4 * (c & 7))) & 0xFu;
 #pragma unroll
-        for (int w = 1; w < 4; ++w)
-          if (x[w][c] > mv) { mv = x[w][c]; arg = w; }
-        const float gg = (mv > 0.f) ? v[c] : 0.f;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) o[w][c] = (w == arg) ? gg : 0.f;
+        for (int w = 0; w < 4; ++w) o[w][c] = ((nib >> w) & 1u) ? v[c] : 0.f;
       }
 #pragma unroll
       for (int w = 0; w < 4; ++w) {
@@ -408,29 +406,47 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
         make_uint4(pack2<DT>(v[0], v[1]), pack2<DT>(v[2], v[3]), pack2<DT>(v[4], v[5]), pack2<DT>(v[6], v[7]));
     const uint4 o1 =
         make_uint4(pack2<DT>(v[8], v[9]), pack2<DT>(v[10], v[11]), pack2<DT>(v[12], v[13]), pack2<DT>(v[14], v[15]));
-    *reinterpret_cast<uint4*>(a.y + off) = o0;
-    *reinterpret_cast<uint4*>(a.y + off + 8) = o1;
+    if (EPI != EPI_POOLFWD || a.y != nullptr) {
+      *reinterpret_cast<uint4*>(a.y + off) = o0;
+      *reinterpret_cast<uint4*>(a.y + off + 8) = o1;
+    }
     if constexpr (EPI == EPI_POOLFWD) {
       // lanes 4q .. 4q+3 hold the window (2 columns x 2 rows) of one pooled pixel: max of the stored
-      // (rounded) values over quad_perm [1,0,3,2] then [2,3,0,1]
-      float r[16];
+      // (rounded) values over quad_perm [1,0,3,2] then [2,3,0,1]; this lane's window position in ATen
+      // order is p = row * 2 + column = (fr & 1) * 2 + ((fr >> 1) & 1)
+      float r[16], own[16];
       unpack8h<DT>(o0, r);
       unpack8h<DT>(o1, r + 8);
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
+        own[c] = r[c];
         float t = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(r[c]), 0xB1, 0xF, 0xF, false));
         r[c] = fmaxf(r[c], t);
         t = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(r[c]), 0x4E, 0xF, 0xF, false));
         r[c] = fmaxf(r[c], t);
+      }
+      uint32_t cw0 = 0u, cw1 = 0u;
+      if (a.codes != nullptr) {
+        const int pbit = 1 << ((fr & 1) * 2 + ((fr >> 1) & 1));
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+          int b = (own[c] == r[c]) ? pbit : 0;
+          b |= __builtin_amdgcn_mov_dpp(b, 0xB1, 0xF, 0xF, false);
+          b |= __builtin_amdgcn_mov_dpp(b, 0x4E, 0xF, 0xF, false);
+          const uint32_t nib = (r[c] > 0.f) ? (uint32_t)(b & -b) : 0u;    // first max, ReLU mask
+          if (c < 8) cw0 |= nib << (4 * c); else cw1 |= nib << (4 * (c - 8));
+        }
       }
       if ((fr & 3) == 0) {
         const int ncb = a.W / (TP / 2);
         const int rp = pt / ncb, cb = pt - rp * ncb;
         const int pr = wp * 64 * PW + i * 16 + fr;
         const int pc = cb * (TP / 4) + (pr >> 4) * 4 + ((pr & 15) >> 2);
-        bf16_t* yp = a.yp + ((size_t)rp * (a.W >> 1) + pc) * a.Cout + chb;
+        const size_t pp = (size_t)rp * (a.W >> 1) + pc;
+        bf16_t* yp = a.yp + pp * a.Cout + chb;
         *reinterpret_cast<uint4*>(yp) = pack8h<DT>(r);
         *reinterpret_cast<uint4*>(yp + 8) = pack8h<DT>(r + 8);
+        if (a.codes != nullptr) *reinterpret_cast<uint2*>(a.codes + pp * (a.Cout >> 3) + (chb >> 3)) = make_uint2(cw0, cw1);
       }
     }
   }
@@ -757,8 +773,9 @@ struct HaloConvArgs {
   const bf16_t* w1 = nullptr;
   const float* b1 = nullptr;
   // EPI_POOLFWD (CO = 64, TCOL = 64; H % 4 == 0, W % 64 == 0): the 2x2/s2 max-pool of the output tile
-  // -> yp [N][H/2][W/2][64]
+  // -> yp [N][H/2][W/2][64], its max-pool codes -> codes [N][H/2][W/2][8] (optional), y optional
   bf16_t* yp = nullptr;
+  uint32_t* codes = nullptr;
 };
 
 template <int DT, int CO, int EPI, int TCOL, int F1 = 0>
@@ -987,8 +1004,10 @@ conv_halo64_kernel(HaloConvArgs a) {
         make_uint4(pack2<DT>(v[0], v[1]), pack2<DT>(v[2], v[3]), pack2<DT>(v[4], v[5]), pack2<DT>(v[6], v[7]));
     const uint4 o1 =
         make_uint4(pack2<DT>(v[8], v[9]), pack2<DT>(v[10], v[11]), pack2<DT>(v[12], v[13]), pack2<DT>(v[14], v[15]));
-    *reinterpret_cast<uint4*>(a.y + off) = o0;
-    *reinterpret_cast<uint4*>(a.y + off + 8) = o1;
+    if (EPI != EPI_POOLFWD || a.y != nullptr) {
+      *reinterpret_cast<uint4*>(a.y + off) = o0;
+      *reinterpret_cast<uint4*>(a.y + off + 8) = o1;
+    }
     if constexpr (EPI == EPI_POOLFWD) {
       // staging tile [4 rows][64 cols] x 128 B, 16-B chunk c of column col at slot c ^ (col & 7)
       const int col = i * 16 + fr;
@@ -1005,21 +1024,26 @@ conv_halo64_kernel(HaloConvArgs a) {
     for (int u = 0; u < 2; ++u) {
       const int o = tid + 256 * u;
       const int c = o & 7, pc = (o >> 3) & 31, pr = o >> 8;
-      float m[8], t[8];
+      float m[8], t[4][8];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < 4; ++q) {     // q = window position in ATen order (row * 2 + column)
         const int rr = 2 * pr + (q >> 1), cc = 2 * pc + (q & 1);
         const uint4 v4 = reinterpret_cast<const uint4*>(halo + (rr * 64 + cc) * 128)[c ^ (cc & 7)];
-        if (q == 0) {
-          unpack8h<DT>(v4, m);
-        } else {
-          unpack8h<DT>(v4, t);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) m[k] = fmaxf(m[k], t[k]);
-        }
+        unpack8h<DT>(v4, t[q]);
       }
-      const size_t po = ((size_t)(n * (a.H >> 1) + (oh0 >> 1) + pr) * (a.W >> 1) + (ow0 >> 1) + pc) * 64 + c * 8;
-      *reinterpret_cast<uint4*>(a.yp + po) = pack8h<DT>(m);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) m[k] = fmaxf(fmaxf(t[0][k], t[1][k]), fmaxf(t[2][k], t[3][k]));
+      const size_t pp = (size_t)(n * (a.H >> 1) + (oh0 >> 1) + pr) * (a.W >> 1) + (ow0 >> 1) + pc;
+      *reinterpret_cast<uint4*>(a.yp + pp * 64 + c * 8) = pack8h<DT>(m);
+      if (a.codes != nullptr) {
+        uint32_t cw = 0u;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t first = (t[0][k] == m[k]) ? 1u : (t[1][k] == m[k]) ? 2u : (t[2][k] == m[k]) ? 4u : 8u;
+          cw |= ((m[k] > 0.f) ? first : 0u) << (4 * k);
+        }
+        a.codes[pp * 8 + c] = cw;
+      }
     }
   }
 }
@@ -1166,6 +1190,9 @@ static int dispatch_glds(const ConvArgs2& a, int tile_cfg, hipStream_t s) {
     const int tp = glds_cfg_tp(cfg);
     if (tp == 0 || (a.H & 1) || a.W % (tp / 2) || a.yp == nullptr) return -12;
   }
+  if constexpr (EPI == EPI_POOLBWD) {
+    if (a.pcodes == nullptr) return -14;
+  }
   switch (cfg) {
     case 11: if (a.Cout % 256 || EPI == EPI_POOLFWD) return -8; return launch_glds<DT, 4, 2, 2, EPI>(a, s);
     case 12: if (a.Cout % 128 || EPI == EPI_POOLFWD) return -8; return launch_glds<DT, 2, 4, 1, EPI>(a, s);
@@ -1240,6 +1267,7 @@ static int conv_igemm_impl(const void* x, const void* w, const float* bias, cons
     ConvArgs2 b;
     b.x = a.x; b.w = a.w; b.bias = a.bias; b.mask = a.mask; b.y = a.y; b.zero = conv_zero_page();
     if (!b.zero) return -10;
+    if (epi == EPI_POOLBWD) { b.mask = nullptr; b.pcodes = (const uint32_t*)mask; }   // mask = max-pool codes
     b.H = H; b.W = W; b.Cin = Cin; b.Cout = Cout; b.ksize = ksize; b.dil = dil; b.M = a.M;
     b.fdW = make_fastdiv((uint32_t)W); b.fdH = make_fastdiv((uint32_t)H);
     switch (epi) {
@@ -1261,25 +1289,27 @@ static int conv_igemm_impl(const void* x, const void* w, const float* bias, cons
   return -6;
 }
 
-// 3x3 / 1x1 conv + bias + ReLU with the 2x2/s2 max-pool fused into the epilogue: y = full-resolution
-// output (kept for the backward pass), yp = pooled output.  LDS-DMA v2 kernels only.
+// 3x3 / 1x1 conv + bias + ReLU with the 2x2/s2 max-pool fused into the epilogue: yp = pooled output,
+// codes = its max-pool codes (what the backward needs), y = the full-resolution output (optional: nullptr
+// skips its 2-byte-per-element store).  LDS-DMA v2 kernels and conv1_2's halo kernel.
 template <int DT>
-static int conv_pool_fwd_impl(const void* x, const void* w, const float* bias, void* y, void* yp, int N, int H,
-                              int W, int Cin, int Cout, int ksize, int dil, int tile_cfg, hipStream_t s) {
+static int conv_pool_fwd_impl(const void* x, const void* w, const float* bias, void* y, void* yp, void* codes,
+                              int N, int H, int W, int Cin, int Cout, int ksize, int dil, int tile_cfg,
+                              hipStream_t s) {
   if (Cout % 64 || Cin % 64 || H < 2 || W < 2) return -3;
   if (Cin == 64 && Cout == 64 && ksize == 3 && dil == 1 && tile_cfg == 0) {
     // conv1_2: halo-tiled kernel, 4 x 64 output tiles (full tiles only: the pool epilogue has barriers)
     if (H % 4 || W % 64) return -13;
     HaloConvArgs h;
     h.x = (const bf16_t*)x; h.w = (const bf16_t*)w; h.bias = bias; h.mask = nullptr; h.y = (bf16_t*)y;
-    h.yp = (bf16_t*)yp; h.zero = conv_zero_page();
+    h.yp = (bf16_t*)yp; h.codes = (uint32_t*)codes; h.zero = conv_zero_page();
     if (!h.zero) return -10;
     h.N = N; h.H = H; h.W = W; h.tiles_x = W / 64; h.tiles_y = H / 4;
     return launch_halo64<DT, 64, EPI_POOLFWD, 64>(h, s);
   }
   ConvArgs2 b;
   b.x = (const bf16_t*)x; b.w = (const bf16_t*)w; b.bias = bias; b.mask = nullptr; b.y = (bf16_t*)y;
-  b.yp = (bf16_t*)yp; b.zero = conv_zero_page();
+  b.yp = (bf16_t*)yp; b.codes = (uint32_t*)codes; b.zero = conv_zero_page();
   if (!b.zero) return -10;
   b.H = H; b.W = W; b.Cin = Cin; b.Cout = Cout; b.ksize = ksize; b.dil = dil; b.M = N * H * W;
   b.fdW = make_fastdiv((uint32_t)W); b.fdH = make_fastdiv((uint32_t)H);
@@ -1317,9 +1347,10 @@ extern "C" int can_conv_igemm(const void* x, const void* w, const float* bias, c
                                               tile_cfg, stream));
 }
 
-extern "C" int can_conv_pool_fwd(const void* x, const void* w, const float* bias, void* y, void* yp, int N, int H,
-                                 int W, int Cin, int Cout, int ksize, int dil, int tile_cfg, int dt, void* stream) {
-  CAN_DT_DISPATCH(dt, can::conv_pool_fwd_impl<DT>(x, w, bias, y, yp, N, H, W, Cin, Cout, ksize, dil, tile_cfg,
+extern "C" int can_conv_pool_fwd(const void* x, const void* w, const float* bias, void* y, void* yp, void* codes,
+                                 int N, int H, int W, int Cin, int Cout, int ksize, int dil, int tile_cfg, int dt,
+                                 void* stream) {
+  CAN_DT_DISPATCH(dt, can::conv_pool_fwd_impl<DT>(x, w, bias, y, yp, codes, N, H, W, Cin, Cout, ksize, dil, tile_cfg,
                                               (hipStream_t)stream));
 }
 

@@ -1263,11 +1263,12 @@ static void wgrad_tile(int cfg, int* TCo, int* TK, int* BKM) {
 }
 
 extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, int target_blocks, int* S_out,
-                              int* mslice_out, int* cfg_out) {
+                              int* mslice_out, int* cfg_out, int dil) {
   const int K = first ? 64 : ksize * ksize * Cin;
   const char* force = getenv("CANNET_WGRAD_CFG");
   int cfg;
-  const bool halo_ok = !first && ksize == 3 && (Cout == 64 || Cout == 128) && Cin % 64 == 0;
+  // the halo weight-gradient kernel is dilation-1 only (B5: 256 -> 128, dil 2, reaches M >= 262144 at batch 32)
+  const bool halo_ok = !first && ksize == 3 && dil == 1 && (Cout == 64 || Cout == 128) && Cin % 64 == 0;
   if (first) cfg = 0;
   else if (halo_ok && getenv("CANNET_NO_HALO") == nullptr && M >= 262144) cfg = 8;
   else if (Cout % 256 == 0 && K >= 2048) cfg = (K % 256 == 0 && getenv("CANNET_WGRAD_V1") == nullptr) ? 9 : 7;

@@ -2,6 +2,8 @@
 // vectorised per lane (8 channels), grid-stride, no atomics on hot paths.
 //
 //   maxpool2x2_fwd      nn.MaxPool2d(2,2)                  model/CANNet.py:112
+//                       (+ optional max-pool codes: first-max one-hots, see conv_igemm.hip)
+//   maxpool2x2_bwd_codes max-pool backward + ReLU mask from the codes alone
 //   maxpool2x2_bwd_relu max_pool2d_with_indices_backward + threshold_backward
 //                       (gather form: first-max-in-window wins, as ATen; the
 //                       ReLU mask of the pooled layer is folded in)
@@ -18,9 +20,11 @@
 namespace can {
 
 // ---------------------------------------------------------------- maxpool
+// codes (optional): per pooled pixel and 8-channel chunk, one uint32 of 4-bit one-hot first-max positions
+// (ATen order, 0 when the max is not > 0) — the layout of the conv pool epilogues (conv_igemm.hip)
 template <int DT>
-__global__ void __launch_bounds__(256) maxpool_fwd_kernel(const uint4* __restrict__ x, uint4* __restrict__ y, int N,
-                                                          int H, int W, int C8) {
+__global__ void __launch_bounds__(256) maxpool_fwd_kernel(const uint4* __restrict__ x, uint4* __restrict__ y,
+                                                          uint32_t* __restrict__ codes, int N, int H, int W, int C8) {
   const int Ho = H >> 1, Wo = W >> 1;
   const size_t total = (size_t)N * Ho * Wo * C8;
   for (size_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
@@ -29,16 +33,52 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const uint4* __restric
     const int ox = p % Wo; p /= Wo;
     const int oy = p % Ho; const int n = p / Ho;
     const size_t base = (((size_t)n * H + 2 * oy) * W + 2 * ox) * C8 + c;
-    float a[8], b[8], m[8];
-    unpack8h<DT>(x[base], m);
-    unpack8h<DT>(x[base + C8], a);
+    float t[4][8], m[8];
+    unpack8h<DT>(x[base], t[0]);
+    unpack8h<DT>(x[base + C8], t[1]);
+    unpack8h<DT>(x[base + (size_t)W * C8], t[2]);
+    unpack8h<DT>(x[base + (size_t)W * C8 + C8], t[3]);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) m[k] = fmaxf(m[k], a[k]);
-    unpack8h<DT>(x[base + (size_t)W * C8], a);
-    unpack8h<DT>(x[base + (size_t)W * C8 + C8], b);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) m[k] = fmaxf(m[k], fmaxf(a[k], b[k]));
+    for (int k = 0; k < 8; ++k) m[k] = fmaxf(fmaxf(t[0][k], t[1][k]), fmaxf(t[2][k], t[3][k]));
     y[i] = pack8h<DT>(m);  // exact: max of bf16 values is a bf16 value
+    if (codes != nullptr) {
+      uint32_t cw = 0u;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t first = (t[0][k] == m[k]) ? 1u : (t[1][k] == m[k]) ? 2u : (t[2][k] == m[k]) ? 4u : 8u;
+        cw |= ((m[k] > 0.f) ? first : 0u) << (4 * k);
+      }
+      codes[i] = cw;
+    }
+  }
+}
+
+// dx[full] = dy[pooled] at the window position the code marks, 0 elsewhere (max-pool backward + the ReLU
+// mask of the pool input, from the codes alone: the pool input is not read)
+template <int DT>
+__global__ void __launch_bounds__(256) maxpool_bwd_codes_kernel(const uint32_t* __restrict__ codes,
+                                                                const uint4* __restrict__ dy, uint4* __restrict__ dx,
+                                                                int N, int H, int W, int C8) {
+  const int Ho = H >> 1, Wo = W >> 1;
+  const size_t total = (size_t)N * Ho * Wo * C8;
+  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const int c = i % C8;
+    size_t p = i / C8;
+    const int ox = p % Wo; p /= Wo;
+    const int oy = p % Ho; const int n = p / Ho;
+    const size_t b0 = (((size_t)n * H + 2 * oy) * W + 2 * ox) * C8 + c;
+    const size_t off[4] = {b0, b0 + C8, b0 + (size_t)W * C8, b0 + (size_t)W * C8 + C8};
+    float g[8], o[4][8];
+    unpack8h<DT>(dy[i], g);
+    const uint32_t cw = codes[i];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t nib = (cw >> (4 * k)) & 0xFu;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q][k] = ((nib >> q) & 1u) ? g[k] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dx[off[q]] = pack8h<DT>(o[q]);
   }
 }
 
@@ -352,11 +392,21 @@ static inline int grid_for(size_t n, int per = 256, int cap = 4096) {
 
 using namespace can;
 
-extern "C" int can_maxpool_fwd(const void* x, void* y, int N, int H, int W, int C, int dt, void* stream) {
+extern "C" int can_maxpool_fwd(const void* x, void* y, void* codes, int N, int H, int W, int C, int dt,
+                               void* stream) {
   if ((C & 7) || (H & 1) || (W & 1)) return -2;
   const size_t tot = (size_t)N * (H / 2) * (W / 2) * (C / 8);
   CAN_LAUNCH_DT(dt, maxpool_fwd_kernel, dim3(grid_for(tot, 256, 8192)), dim3(256), 0,
-                (hipStream_t)stream, (const uint4*)x, (uint4*)y, N, H, W, C / 8);
+                (hipStream_t)stream, (const uint4*)x, (uint4*)y, (uint32_t*)codes, N, H, W, C / 8);
+  return (int)hipGetLastError();
+}
+
+extern "C" int can_maxpool_bwd_codes(const void* codes, const void* dy, void* dx, int N, int H, int W, int C, int dt,
+                                     void* stream) {
+  if ((C & 7) || (H & 1) || (W & 1)) return -2;
+  const size_t tot = (size_t)N * (H / 2) * (W / 2) * (C / 8);
+  CAN_LAUNCH_DT(dt, maxpool_bwd_codes_kernel, dim3(grid_for(tot, 256, 8192)), dim3(256), 0,
+                (hipStream_t)stream, (const uint32_t*)codes, (const uint4*)dy, (uint4*)dx, N, H, W, C / 8);
   return (int)hipGetLastError();
 }
 

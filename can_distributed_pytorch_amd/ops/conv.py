@@ -78,8 +78,9 @@ def conv_igemm(x: torch.Tensor, wpack: torch.Tensor, bias: Optional[torch.Tensor
                first: bool = False, tile: int = 0) -> torch.Tensor:
     """y[N,H,W,Co] = epi(conv(x[N,H,W,Ci], W) ...), stride 1, 'same' padding = dil*(ksize//2).
 
-    epi=EPI_POOLBWD: the conv result is d(maxpool output); ``mask`` is the 2x2/s2 max-pool INPUT
-    [N,2H,2W,Co] and the result is written as d(pool input) * (pool max > 0) into [N,2H,2W,Co]."""
+    epi=EPI_POOLBWD: the conv result is d(maxpool output); ``mask`` is the pool's max-pool codes
+    (int32 [N,H,W,Co/8], see ``maxpool_codes``) and the result is written as d(pool input) (ReLU mask of the
+    pool input included) into [N,2H,2W,Co]."""
     C = _ext.require()
     if x.dim() != 4:
         raise ValueError("x must be [N,H,W,C]")
@@ -105,11 +106,13 @@ def conv_igemm(x: torch.Tensor, wpack: torch.Tensor, bias: Optional[torch.Tensor
         if bias is None or bias.dtype != torch.float32 or bias.numel() != co or not bias.is_contiguous():
             raise ValueError("bias must be contiguous fp32 [Cout]")
     oshape = (n, 2 * h, 2 * w, co) if epi == EPI_POOLBWD else (n, h, w, co)
-    if epi in (EPI_MASK, EPI_POOLBWD):
+    if epi == EPI_MASK:
         if mask is None or tuple(mask.shape) != oshape:
             raise ValueError(f"mask must be {list(oshape)}")
         _check_act(mask, "mask", dtype=dt)
-        if epi == EPI_POOLBWD and (first or tile not in (0, 21, 22, 23, 25)):
+    if epi == EPI_POOLBWD:
+        _check_codes(mask, (n, h, w, co))
+        if first or tile not in (0, 21, 22, 23, 25):
             raise ValueError("EPI_POOLBWD runs on the LDS-DMA kernels only")
     if out is None:
         out = torch.empty(*oshape, dtype=dt, device=x.device)
@@ -125,6 +128,44 @@ def conv_igemm(x: torch.Tensor, wpack: torch.Tensor, bias: Optional[torch.Tensor
     return out
 
 
+def _check_codes(codes: Optional[torch.Tensor], pooled_shape) -> None:
+    n, h, w, c = pooled_shape
+    if codes is None or codes.dtype != torch.int32 or not codes.is_cuda or not codes.is_contiguous() or \
+            tuple(codes.shape) != (n, h, w, c // 8):
+        raise ValueError(f"max-pool codes must be a contiguous int32 GPU tensor [{n},{h},{w},{c // 8}]")
+
+
+def maxpool_codes(x: torch.Tensor):
+    """2x2/s2 max-pool of x [N,H,W,C] -> (pooled [N,H/2,W/2,C], codes int32 [N,H/2,W/2,C/8]).
+
+    codes: per pooled pixel and channel a 4-bit one-hot of the FIRST max of its window (ATen scan order
+    (0,0),(0,1),(1,0),(1,1) = bits 0..3), 0 when that max is not > 0 (the ReLU mask of the pool input);
+    channel c sits in word c // 8, nibble c % 8.  The backward (``maxpool_bwd_codes``, EPI_POOLBWD) needs
+    nothing else, so the pool input need not be kept."""
+    C = _ext.require()
+    _check_act(x, "x")
+    n, h, w, c = x.shape
+    if h % 2 or w % 2 or c % 8:
+        raise ValueError("max-pool needs even H, W and C % 8 == 0")
+    y = torch.empty(n, h // 2, w // 2, c, dtype=x.dtype, device=x.device)
+    codes = torch.empty(n, h // 2, w // 2, c // 8, dtype=torch.int32, device=x.device)
+    C.maxpool_fwd(x.data_ptr(), y.data_ptr(), n, h, w, c, dt_code(x.dtype), _ext.stream_ptr(x.device),
+                  codes.data_ptr())
+    return y, codes
+
+
+def maxpool_bwd_codes(codes: torch.Tensor, dy: torch.Tensor) -> torch.Tensor:
+    """d(pool input) [N,2H,2W,C] from d(pool output) dy [N,H,W,C] and the pool's codes."""
+    C = _ext.require()
+    _check_act(dy, "dy")
+    n, h, w, c = dy.shape
+    _check_codes(codes, (n, h, w, c))
+    dx = torch.empty(n, 2 * h, 2 * w, c, dtype=dy.dtype, device=dy.device)
+    C.maxpool_bwd_codes(codes.data_ptr(), dy.data_ptr(), dx.data_ptr(), n, 2 * h, 2 * w, c, dt_code(dy.dtype),
+                        _ext.stream_ptr(dy.device))
+    return dx
+
+
 class WgradWorkspace:
     """One fp32 scratch buffer for the split-pixel partial slabs, grown on demand
     (allocated outside any captured region, never inside a launch function)."""
@@ -134,9 +175,9 @@ class WgradWorkspace:
         self.target_blocks = target_blocks
         self.buf = torch.empty(0, dtype=torch.float32, device=self.device)
 
-    def plan(self, m: int, ci: int, co: int, ksize: int, first: bool):
+    def plan(self, m: int, ci: int, co: int, ksize: int, first: bool, dil: int = 1):
         C = _ext.require()
-        s, mslice, cfg = C.wgrad_plan(m, ci, co, ksize, int(first), self.target_blocks)
+        s, mslice, cfg = C.wgrad_plan(m, ci, co, ksize, int(first), self.target_blocks, dil)
         ktot = 64 if first else ksize * ksize * ci
         need = s * ktot * co + max(s, 512) * co      # slabs + bias partials (v2 path: 512 column-sum parts)
         return s, mslice, cfg, need
@@ -174,7 +215,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, db: Optional
     if db is not None and (db.dtype != torch.float32 or db.numel() != co or not db.is_contiguous()):
         raise ValueError("db must be contiguous fp32 [Co]")
     ws = ws or WgradWorkspace(x.device)
-    s, mslice, cfg, need = ws.plan(n * h * w, ci, co, ksize, first)
+    s, mslice, cfg, need = ws.plan(n * h * w, ci, co, ksize, first, dil)
     buf = ws.reserve(need)
     ktot = 64 if first else ksize * ksize * ci
     wsb_ptr = buf.data_ptr() + 4 * s * ktot * co
@@ -263,9 +304,12 @@ def conv_pool_fwd_ok(x: torch.Tensor, cout: int, ksize: int, tile: int = 0) -> b
 
 
 def conv_pool_fwd(x: torch.Tensor, wpack: torch.Tensor, bias: torch.Tensor, *, ksize: int, dil: int = 1,
-                  out: Optional[torch.Tensor] = None, pooled: Optional[torch.Tensor] = None, tile: int = 0):
-    """relu(conv(x, W) + b) -> (y [N,H,W,Co], maxpool2x2(y) [N,H/2,W/2,Co]) in one kernel: the pool runs in the
-    conv epilogue on the rounded outputs, so both tensors equal conv_igemm(EPI_BIAS_RELU) + maxpool_fwd bitwise."""
+                  out: Optional[torch.Tensor] = None, pooled: Optional[torch.Tensor] = None, tile: int = 0,
+                  keep_full: bool = True, codes: bool = False):
+    """relu(conv(x, W) + b) -> (y [N,H,W,Co] or None, maxpool2x2(y) [N,H/2,W/2,Co], codes or None) in one kernel:
+    the pool runs in the conv epilogue on the rounded outputs, so the tensors equal conv_igemm(EPI_BIAS_RELU) +
+    maxpool_codes bitwise.  keep_full=False skips the full-resolution store (the training step keeps only the
+    pooled map and the max-pool codes its backward needs)."""
     C = _ext.require()
     _check_act(x, "x")
     n, h, w, ci = x.shape
@@ -279,18 +323,22 @@ def conv_pool_fwd(x: torch.Tensor, wpack: torch.Tensor, bias: torch.Tensor, *, k
         raise ValueError(f"fused pool needs H even and W a multiple of the tile half-width ({list(x.shape)})")
     if n * h * w >= 2 ** 31 // max(ci, co):
         raise ValueError("tensor too large for 32-bit pixel indexing")
+    if not keep_full and out is not None:
+        raise ValueError("out given with keep_full=False")
     for t, shp, name in ((out, (n, h, w, co), "out"), (pooled, (n, h // 2, w // 2, co), "pooled")):
         if t is not None:
             if tuple(t.shape) != shp:
                 raise ValueError(f"{name} must be {list(shp)}")
             _check_act(t, name, dtype=dt)
-    if out is None:
+    if out is None and keep_full:
         out = torch.empty(n, h, w, co, dtype=dt, device=x.device)
     if pooled is None:
         pooled = torch.empty(n, h // 2, w // 2, co, dtype=dt, device=x.device)
-    C.conv_pool_fwd(x.data_ptr(), wpack.data_ptr(), bias.data_ptr(), out.data_ptr(), pooled.data_ptr(), n, h, w, ci,
-                    co, ksize, dil, tile, dt_code(dt), _ext.stream_ptr(x.device))
-    return out, pooled
+    cd = torch.empty(n, h // 2, w // 2, co // 8, dtype=torch.int32, device=x.device) if codes else None
+    C.conv_pool_fwd(x.data_ptr(), wpack.data_ptr(), bias.data_ptr(), out.data_ptr() if out is not None else 0,
+                    pooled.data_ptr(), cd.data_ptr() if cd is not None else 0, n, h, w, ci, co, ksize, dil, tile,
+                    dt_code(dt), _ext.stream_ptr(x.device))
+    return out, pooled, cd
 
 
 def conv_f1(x: Optional[torch.Tensor], wpack: torch.Tensor, bias: Optional[torch.Tensor], img: torch.Tensor,

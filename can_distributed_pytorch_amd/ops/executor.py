@@ -11,7 +11,9 @@ master weights in the model's own nn.Parameters, 16-bit packed weight copies
 fp32 weights change.
 
 Forward (training) saves exactly what the backward needs: every conv input
-(NHWC bf16), the pre-pool activations, the context tables, c_S and w_S.
+(NHWC bf16), the max-pool codes of the three pools (4-bit first-max one-hots:
+the full-resolution pre-pool activations are never stored), the context
+tables, c_S and w_S.
 Backward (per layer, reverse order) = weight-gradient (split-pixel MFMA +
 deterministic slab reduction) + data-gradient (same MFMA kernel as forward,
 flipped weights, ReLU mask / maxpool-backward fused), and after each layer's
@@ -177,7 +179,7 @@ class CANNetExecutor:
             if s.pool_after:
                 hh, ww = hh // 2, ww // 2
         for s in self.back:
-            need = max(need, self.ws.plan(n * hh * ww, s.cin, s.cout, 3, False)[3])
+            need = max(need, self.ws.plan(n * hh * ww, s.cin, s.cout, 3, False, s.dil)[3])
         need = max(need, self.ws.plan(n * hh * ww, 512, 512, 1, False)[3])
         need = max(need, C.wgrad_1x1_batched_plan(n * hh * ww, 4, 512, 512)[2])
         need = max(need, C.conv_wgrad_f1_need(n * h * w))
@@ -196,10 +198,12 @@ class CANNetExecutor:
                 and os.environ.get("CANNET_POOL_FWD_FUSED", "1") != "0" and C.conv_pool_fwd_ok(x, s.cout, s.ksize))
 
     def _maxpool(self, x):
+        """(pooled, max-pool codes): the codes replace the pool input in the saved state."""
         n, h, w, c = x.shape
         y = torch.empty(n, h // 2, w // 2, c, dtype=self.act, device=x.device)
-        self.C.maxpool_fwd(x.data_ptr(), y.data_ptr(), n, h, w, c, self.dt, self._stream())
-        return y
+        codes = torch.empty(n, h // 2, w // 2, c // 8, dtype=torch.int32, device=x.device)
+        self.C.maxpool_fwd(x.data_ptr(), y.data_ptr(), n, h, w, c, self.dt, self._stream(), codes.data_ptr())
+        return y, codes
 
     def _img(self, img):
         if img.dim() == 4 and img.shape[-1] == 4 and img.dtype in C.ACT_DTYPES:
@@ -249,15 +253,19 @@ class CANNetExecutor:
                 fwd, _ = self.packs[id(s.module.weight)]
                 y = C.conv_f1(None, fwd, s.module.bias.detach(), acts[0], w1, b1, epi=C.EPI_BIAS_RELU)
             elif self._pool_fused(s, x):
+                # conv + ReLU + pool in one kernel; only the pooled map and the max-pool codes are written
+                # (the full-resolution output is never stored: the backward needs the codes alone)
                 fwd, _ = self.packs[id(s.module.weight)]
-                y, x = C.conv_pool_fwd(x, fwd, s.module.bias.detach(), ksize=s.ksize, dil=s.dil)
-                pre_pool[s.idx] = y
+                _, x, codes = C.conv_pool_fwd(x, fwd, s.module.bias.detach(), ksize=s.ksize, dil=s.dil,
+                                              keep_full=False, codes=save)
+                if save:
+                    pre_pool[s.idx] = codes
                 continue
             else:
                 y = self._conv(s, x)
             if s.pool_after:
-                pre_pool[s.idx] = y
-                x = self._maxpool(y)
+                x, codes = self._maxpool(y)
+                pre_pool[s.idx] = codes
             else:
                 x = y
         fv = x
@@ -371,15 +379,12 @@ class CANNetExecutor:
                 # data gradient at the pooled resolution, scattered through the max-pool backward
                 # (+ ReLU mask of the pool input) in the conv epilogue: the pooled gradient never
                 # round-trips through memory
-                full = sv["pre_pool"][prev.idx]
+                codes = sv["pre_pool"][prev.idx]
                 if os.environ.get("CANNET_POOLBWD_FUSED", "1") != "0":
-                    dy = C.conv_igemm(dy, dgr, None, ksize=3, dil=1, epi=C.EPI_POOLBWD, mask=full)
+                    dy = C.conv_igemm(dy, dgr, None, ksize=3, dil=1, epi=C.EPI_POOLBWD, mask=codes)
                 else:
                     dp = C.conv_igemm(dy, dgr, None, ksize=3, dil=1, epi=C.EPI_NONE)
-                    dy = torch.empty_like(full)
-                    nn_, hh, ww, cc = full.shape
-                    self.C.maxpool_bwd_relu(full.data_ptr(), dp.data_ptr(), dy.data_ptr(), nn_, hh, ww, cc, self.dt,
-                                            st)
+                    dy = C.maxpool_bwd_codes(codes, dp)
             else:
                 dy = C.conv_igemm(dy, dgr, None, ksize=3, dil=1, epi=C.EPI_MASK, mask=x)
         if side is not None:

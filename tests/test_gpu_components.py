@@ -29,6 +29,15 @@ def test_maxpool_fwd_bwd():
     C.maxpool_bwd_relu(x.data_ptr(), g.data_ptr(), dx.data_ptr(), n, h, w, c, 0, _ext.stream_ptr())
     torch.cuda.synchronize()
     assert torch.equal(dx.float(), ref)
+    # max-pool codes: the backward from the codes alone (the pool input is not kept) is the same map
+    from can_distributed_pytorch_amd.ops import conv as CV
+    x[:, ::2, ::2, ::3] = 0                                   # ties (first max wins) and zero windows
+    y2, codes = CV.maxpool_codes(x)
+    assert torch.equal(y2.float(), F.max_pool2d(x.float().permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1))
+    dx2 = CV.maxpool_bwd_codes(codes, g)
+    C.maxpool_bwd_relu(x.data_ptr(), g.data_ptr(), dx.data_ptr(), n, h, w, c, 0, _ext.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(dx2, dx)
 
 
 def _ctx_ref(fv, w1, w2):

@@ -225,12 +225,16 @@ def test_conv_pool_fwd_fused(n, h, w, ci, co, dil, dtype):
     b = torch.randn(co, device="cuda") * 0.1
     wp = C.pack_weight_fwd(wt, dtype)
     assert C.conv_pool_fwd_ok(x, co, 3)
-    y, yp = C.conv_pool_fwd(x, wp, b, ksize=3, dil=dil)
+    y, yp, codes = C.conv_pool_fwd(x, wp, b, ksize=3, dil=dil, codes=True)
+    _, yp2, codes2 = C.conv_pool_fwd(x, wp, b, ksize=3, dil=dil, keep_full=False, codes=True)
     y_ref = C.conv_igemm(x, wp, b, ksize=3, dil=dil)
     yp_ref = F.max_pool2d(y_ref.permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1).contiguous()
+    yp_ref2, codes_ref = C.maxpool_codes(y_ref)
     torch.cuda.synchronize()
     assert torch.equal(y, y_ref)
-    assert torch.equal(yp, yp_ref)
+    assert torch.equal(yp, yp_ref) and torch.equal(yp_ref2, yp_ref)
+    assert torch.equal(codes, codes_ref)
+    assert torch.equal(yp2, yp) and torch.equal(codes2, codes)       # without the full-resolution store
     assert not C.conv_pool_fwd_ok(x[:, :h - 1].contiguous(), co, 3)     # odd H: not covered
     if ci == 64 and co == 64:                                            # halo kernel: whole 4-row tiles
         assert not C.conv_pool_fwd_ok(x[:, :h - 2].contiguous(), co, 3)
@@ -267,7 +271,8 @@ def test_wgrad_tiled_reduction_matches_grid_stride(n, h, w, ci, co, dil, beta, m
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("n,h,w,ci,co", [(2, 12, 20, 128, 64), (1, 9, 13, 256, 128), (2, 6, 8, 512, 256)])
 def test_conv_dgrad_pool_backward_fused(n, h, w, ci, co, dtype):
-    """EPI_POOLBWD (dgrad + max-pool backward + ReLU mask in one epilogue) == EPI_NONE + maxpool_bwd_relu, bitwise."""
+    """EPI_POOLBWD (dgrad + max-pool backward + ReLU mask in one epilogue, driven by the max-pool codes) ==
+    EPI_NONE + maxpool_bwd_codes == EPI_NONE + maxpool_bwd_relu on the pool input itself, bitwise."""
     from can_distributed_pytorch_amd.ops import _ext
     from can_distributed_pytorch_amd.ops import conv as C
     torch.manual_seed(9)
@@ -275,13 +280,16 @@ def test_conv_dgrad_pool_backward_fused(n, h, w, ci, co, dtype):
     dy = torch.randn(n, h, w, ci, device="cuda").to(dtype)
     full = torch.relu(torch.randn(n, 2 * h, 2 * w, co, device="cuda")).to(dtype)
     full[:, ::3, ::2] = 0                                          # ties and all-zero windows
+    _, codes = C.maxpool_codes(full)
     pack = C.pack_weight_dgrad(wt, dtype)
-    fused = C.conv_igemm(dy, pack, None, ksize=3, epi=C.EPI_POOLBWD, mask=full)
+    fused = C.conv_igemm(dy, pack, None, ksize=3, epi=C.EPI_POOLBWD, mask=codes)
     dp = C.conv_igemm(dy, pack, None, ksize=3, epi=C.EPI_NONE)
+    via_codes = C.maxpool_bwd_codes(codes, dp)
     ref = torch.empty_like(full)
     _ext.require().maxpool_bwd_relu(full.data_ptr(), dp.data_ptr(), ref.data_ptr(), n, 2 * h, 2 * w, co,
                                     C.dt_code(dtype), _ext.stream_ptr())
     torch.cuda.synchronize()
+    assert torch.equal(via_codes, ref)
     assert torch.equal(fused, ref)
 
 
