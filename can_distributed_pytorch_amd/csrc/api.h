@@ -8,14 +8,17 @@ extern "C" {
 #endif
 
 int can_conv_igemm(const void* x, const void* w, const float* bias, const void* mask, void* y, int N, int H, int W,
-                   int Cin, int Cout, int ksize, int dil, int epi, int first, int tile_cfg, int dt, void* stream);
+                   int Cin, int Cout, int ksize, int dil, int epi, int first, int tile_cfg, int dt, void* stream,
+                   float* bpart, int bpart_cap, int* bpart_rows);
 
 int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, int target_blocks, int* S_out, int* mslice_out,
                    int* cfg_out, int dil);
 int can_conv_wgrad(const void* dy, const void* x, float* ws, float* wsb, float* dw, float* db, int N, int H, int W,
                    int Cin, int Cout, int ksize, int dil, int first, int S, int mslice, int cfg, float beta,
-                   float scale, const float* dscale, int dt, void* stream);
+                   float scale, const float* dscale, int dt, void* stream, const float* bext, int bext_rows);
 
+// [R][C] fp32 rows -> <= rows_out rows (fixed-order block sums); returns the rows written (< 0: error)
+int can_bias_rows_reduce(const float* in, float* out, int R, int C, int rows_out, void* stream);
 int can_conv_wgrad_1x1_batched(const void* dy, const void* x, float* ws, float* dw, int M, int W, int Cin, int Cout,
                                int nb, long long dy_bs, long long x_bs, long long dw_bs, int S, int mslice, float beta,
                                float scale, const float* dscale, int dt, void* stream);
@@ -65,11 +68,18 @@ int can_ctx_bwd_final(const void* dcat, const void* dc, const float* dave, const
                       int w, int C, int dt, void* stream);
 
 // density.hip
-int can_density_map(const float* pts, int n, int H, int W, float* sigma_ws, float* out, int max_r, void* stream);
+int can_density_map(const float* pts, int n, int H, int W, float* sigma_ws, float* out, int max_r, void* stream,
+                    float fixed_sigma);
 
 // preprocess.hip
 int can_preprocess_image(const void* img, int H0, int W0, int C, int flip, void* out, int Ho, int Wo, int dt,
                          void* stream);
+// one launch per batch: packed uint8 images / fp32 densities, desc [n][8] int64 (device)
+int can_preprocess_batch(const void* imgs, const float* dens, const long long* desc, int n, void* x4, float* gt,
+                         int Ho, int Wo, int ds, int dt, void* stream);
+// synthetic batch: full-res densities [n][H][W] + coarse noise [n][3][H/16][W/16] -> x4 NHWC4, gt [n][H/8][W/8]
+int can_synth_render(const float* dens, const float* noise, float* dmax, void* x4, float* gt, int n, int H, int W,
+                     int dt, void* stream);
 int can_preprocess_density(const float* d, int H0, int W0, int flip, float* out, int Ho, int Wo, float mult,
                            void* stream);
 

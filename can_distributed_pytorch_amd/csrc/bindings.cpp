@@ -42,11 +42,16 @@ PYBIND11_MODULE(CAN_MODULE_NAME, m) {
   });
 
   m.def("conv_igemm", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t mask, uintptr_t y, int N, int H, int W,
-                         int Cin, int Cout, int ksize, int dil, int epi, int first, int tile_cfg, int dt, uintptr_t stream) {
+                         int Cin, int Cout, int ksize, int dil, int epi, int first, int tile_cfg, int dt, uintptr_t stream,
+                         uintptr_t bpart, int bpart_cap) {
+    int rows = 0;
     check(can_conv_igemm(P(x), P(w), (const float*)bias, P(mask), P(y), N, H, W, Cin, Cout, ksize, dil, epi, first,
-                         tile_cfg, dt, P(stream)),
+                         tile_cfg, dt, P(stream), (float*)bpart, bpart_cap, &rows),
           "conv_igemm");
-  });
+    return rows;
+  }, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("mask"), py::arg("y"), py::arg("N"), py::arg("H"),
+     py::arg("W"), py::arg("Cin"), py::arg("Cout"), py::arg("ksize"), py::arg("dil"), py::arg("epi"), py::arg("first"),
+     py::arg("tile_cfg"), py::arg("dt"), py::arg("stream"), py::arg("bpart") = 0, py::arg("bpart_cap") = 0);
 
   m.def("wgrad_plan", [](int M, int Cin, int Cout, int ksize, int first, int target_blocks, int dil) {
     int S = 0, ms = 0, cfg = 0;
@@ -56,12 +61,22 @@ PYBIND11_MODULE(CAN_MODULE_NAME, m) {
      py::arg("dil") = 1);
   m.def("conv_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t ws, uintptr_t wsb, uintptr_t dw, uintptr_t db, int N,
                          int H, int W, int Cin, int Cout, int ksize, int dil, int first, int S, int mslice, int cfg,
-                         float beta, float scale, uintptr_t dscale, int dt, uintptr_t stream) {
+                         float beta, float scale, uintptr_t dscale, int dt, uintptr_t stream, uintptr_t bext,
+                         int bext_rows) {
     check(can_conv_wgrad(P(dy), P(x), (float*)ws, (float*)wsb, (float*)dw, (float*)db, N, H, W, Cin, Cout, ksize, dil,
-                         first, S, mslice, cfg, beta, scale, (const float*)dscale, dt, P(stream)),
+                         first, S, mslice, cfg, beta, scale, (const float*)dscale, dt, P(stream), (const float*)bext,
+                         bext_rows),
           "conv_wgrad");
-  });
+  }, py::arg("dy"), py::arg("x"), py::arg("ws"), py::arg("wsb"), py::arg("dw"), py::arg("db"), py::arg("N"),
+     py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("Cout"), py::arg("ksize"), py::arg("dil"), py::arg("first"),
+     py::arg("S"), py::arg("mslice"), py::arg("cfg"), py::arg("beta"), py::arg("scale"), py::arg("dscale"),
+     py::arg("dt"), py::arg("stream"), py::arg("bext") = 0, py::arg("bext_rows") = 0);
 
+  m.def("bias_rows_reduce", [](uintptr_t in, uintptr_t out, int R, int C, int rows_out, uintptr_t st) {
+    const int g = can_bias_rows_reduce((const float*)in, (float*)out, R, C, rows_out, P(st));
+    if (g < 0) check(g, "bias_rows_reduce");
+    return g;
+  });
   m.def("conv_wgrad_1x1_batched", [](uintptr_t dy, uintptr_t x, uintptr_t ws, uintptr_t dw, int M, int W, int Cin,
                                      int Cout, int nb, long long dy_bs, long long x_bs, long long dw_bs, int S,
                                      int mslice, float beta, float scale, uintptr_t dscale, int dt, uintptr_t stream) {
@@ -176,13 +191,28 @@ PYBIND11_MODULE(CAN_MODULE_NAME, m) {
           "ctx_bwd_final");
   });
   // ---- density maps
-  m.def("density_map", [](uintptr_t pts, int n, int H, int W, uintptr_t sig, uintptr_t out, int max_r, uintptr_t st) {
-    check(can_density_map((const float*)pts, n, H, W, (float*)sig, (float*)out, max_r, P(st)), "density_map");
-  });
+  m.def("density_map", [](uintptr_t pts, int n, int H, int W, uintptr_t sig, uintptr_t out, int max_r, uintptr_t st,
+                          float fixed_sigma) {
+    check(can_density_map((const float*)pts, n, H, W, (float*)sig, (float*)out, max_r, P(st), fixed_sigma),
+          "density_map");
+  }, py::arg("pts"), py::arg("n"), py::arg("H"), py::arg("W"), py::arg("sig"), py::arg("out"), py::arg("max_r"),
+     py::arg("st"), py::arg("fixed_sigma") = 0.f);
   // ---- input pipeline
   m.def("preprocess_image", [](uintptr_t img, int H0, int W0, int C, int flip, uintptr_t out, int Ho, int Wo, int dt,
                                uintptr_t st) {
     check(can_preprocess_image(P(img), H0, W0, C, flip, P(out), Ho, Wo, dt, P(st)), "preprocess_image");
+  });
+  m.def("preprocess_batch", [](uintptr_t imgs, uintptr_t dens, uintptr_t desc, int n, uintptr_t x4, uintptr_t gt,
+                               int Ho, int Wo, int ds, int dt, uintptr_t st) {
+    check(can_preprocess_batch(P(imgs), (const float*)dens, (const long long*)desc, n, P(x4), (float*)gt, Ho, Wo, ds,
+                               dt, P(st)),
+          "preprocess_batch");
+  });
+  m.def("synth_render", [](uintptr_t dens, uintptr_t noise, uintptr_t dmax, uintptr_t x4, uintptr_t gt, int n, int H,
+                           int W, int dt, uintptr_t st) {
+    check(can_synth_render((const float*)dens, (const float*)noise, (float*)dmax, P(x4), (float*)gt, n, H, W, dt,
+                           P(st)),
+          "synth_render");
   });
   m.def("preprocess_density", [](uintptr_t d, int H0, int W0, int flip, uintptr_t out, int Ho, int Wo, float mult,
                                  uintptr_t st) {

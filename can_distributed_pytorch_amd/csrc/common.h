@@ -134,6 +134,33 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// Bias-gradient partials from a conv epilogue: lane (fr = lane & 15, fq = lane >> 4) holds 16 per-channel
+// sums bs[0..15] over its pixels; the 16 lanes of a row (same fq, same channels) are summed by a
+// transposing butterfly (each xor round halves the channels a lane keeps: 15 swaps instead of 64), after
+// which lane fr holds the total of channel fr, and the 64 lanes store 64 consecutive floats
+// part[chb0 + fq * 16 + fr].  Fixed order: deterministic.
+__device__ __forceinline__ void store_bias_partials(float (&bs)[16], float* __restrict__ part, int fr) {
+  float t8[8], t4[4], t2[2];
+  const bool h8 = fr & 8, h4 = fr & 4, h2 = fr & 2, h1 = fr & 1;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float send = h8 ? bs[j] : bs[j + 8];
+    t8[j] = (h8 ? bs[j + 8] : bs[j]) + __shfl_xor(send, 8, 64);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float send = h4 ? t8[j] : t8[j + 4];
+    t4[j] = (h4 ? t8[j + 4] : t8[j]) + __shfl_xor(send, 4, 64);
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const float send = h2 ? t4[j] : t4[j + 2];
+    t2[j] = (h2 ? t4[j + 2] : t4[j]) + __shfl_xor(send, 2, 64);
+  }
+  const float send = h1 ? t2[0] : t2[1];
+  part[fr] = (h1 ? t2[1] : t2[0]) + __shfl_xor(send, 1, 64);
+}
+
 // A-operand row order of the 16x16x32 MFMA convs: LDS / fragment row rho -> output channel, so
 // that lane q of the D layout (rows q*4+r of tile jt) owns channels q*16 + jt*4 + r, i.e. 16
 // CONSECUTIVE channels of one pixel per lane (two 16-B stores, no LDS round trip in epilogues).

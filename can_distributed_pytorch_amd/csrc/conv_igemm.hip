@@ -315,6 +315,9 @@ struct ConvArgs2 {
   bf16_t* yp = nullptr;   // EPI_POOLFWD: pooled output [N][H/2][W/2][Cout]
   uint32_t* codes = nullptr;         // EPI_POOLFWD: max-pool codes (optional); a.y optional too
   const uint32_t* pcodes = nullptr;  // EPI_POOLBWD: max-pool codes of the pool this gradient goes through
+  // EPI_MASK / EPI_POOLBWD (data gradient = the next layer's dY): bias-gradient partials of that dY,
+  // [npt * WP][Cout] fp32, row = pixel tile * WP + wave's pixel slot (optional)
+  float* bpart = nullptr;
 };
 
 // pixel m of row r of pixel tile pt; EPI_POOLFWD tiles are 2 rows x TP/2 columns, rows interleaved per
@@ -345,6 +348,10 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
       bias[c] = b4.x; bias[c + 1] = b4.y; bias[c + 2] = b4.z; bias[c + 3] = b4.w;
     }
   }
+  constexpr bool BPART = (EPI == EPI_MASK || EPI == EPI_POOLBWD);
+  float bs[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) bs[c] = 0.f;
 #pragma unroll
   for (int i = 0; i < 4 * PW; ++i) {
     const int m = tile_pix<TP, EPI>(a, pt, wp * 64 * PW + i * 16 + fr);
@@ -371,6 +378,7 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
         const unsigned nib = ((c < 8 ? cw.x : cw.y) >> (4 * (c & 7))) & 0xFu;
 #pragma unroll
         for (int w = 0; w < 4; ++w) o[w][c] = ((nib >> w) & 1u) ? v[c] : 0.f;
+        if (nib) bs[c] += v[c];
       }
 #pragma unroll
       for (int w = 0; w < 4; ++w) {
@@ -400,6 +408,7 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
         const unsigned short bits = (unsigned short)(mw[c >> 1] >> ((c & 1) * 16));
         const bool pos = pos_bits(bits);
         v[c] = pos ? v[c] : 0.f;
+        bs[c] += v[c];
       }
     }
     const uint4 o0 =
@@ -449,6 +458,9 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
         if (a.codes != nullptr) *reinterpret_cast<uint2*>(a.codes + pp * (a.Cout >> 3) + (chb >> 3)) = make_uint2(cw0, cw1);
       }
     }
+  }
+  if constexpr (BPART) {
+    if (a.bpart != nullptr) store_bias_partials(bs, a.bpart + (size_t)(pt * WP + wp) * a.Cout + chb, fr);
   }
 }
 
@@ -776,6 +788,8 @@ struct HaloConvArgs {
   // -> yp [N][H/2][W/2][64], its max-pool codes -> codes [N][H/2][W/2][8] (optional), y optional
   bf16_t* yp = nullptr;
   uint32_t* codes = nullptr;
+  // EPI_MASK (not F1): bias-gradient partials of the produced dY, [ntile * rows per tile][CO] fp32
+  float* bpart = nullptr;
 };
 
 template <int DT, int CO, int EPI, int TCOL, int F1 = 0>
@@ -939,11 +953,26 @@ conv_halo64_kernel(HaloConvArgs a) {
 
   // ---- epilogue: lane owns 16 consecutive channels of one pixel per fragment
   const int oh = oh0 + r;
+  const int chb = wc * 64 + fq * 16;
+  constexpr bool BPART = (EPI == EPI_MASK && !F1);
+  // bias partials: row = tile * (NW * 64 / CO) + this wave's (row, column-half) slot, written even by a
+  // wave whose row is outside the image (zeros)
+  float bs[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) bs[c] = 0.f;
+  auto flush_bias = [&]() {
+    if constexpr (BPART) {
+      if (a.bpart != nullptr)
+        store_bias_partials(bs, a.bpart + ((size_t)tile * (NW * 64 / CO) + wave / (CO / 64)) * CO + chb, fr);
+    }
+  };
   // fused pool: every wave's tap reads are done before the halo region becomes the output staging tile
   // (the host guarantees full tiles, so no wave leaves before the barriers)
   if constexpr (EPI == EPI_POOLFWD) __syncthreads();
-  if (oh >= a.H) return;
-  const int chb = wc * 64 + fq * 16;
+  if (oh >= a.H) {
+    flush_bias();
+    return;
+  }
   float bias[16];
   if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS || EPI == EPI_POOLFWD || (F1 && EPI == EPI_MASK)) {
     const float* bsrc = (F1 && EPI == EPI_MASK) ? a.b1 : a.bias;   // F1 mask: conv1_1's bias
@@ -998,6 +1027,7 @@ conv_halo64_kernel(HaloConvArgs a) {
         const unsigned short bits = (unsigned short)(mw[c >> 1] >> ((c & 1) * 16));
         const bool pos = pos_bits(bits);
         v[c] = pos ? v[c] : 0.f;
+        bs[c] += v[c];
       }
     }
     const uint4 o0 =
@@ -1046,6 +1076,7 @@ conv_halo64_kernel(HaloConvArgs a) {
       }
     }
   }
+  flush_bias();
 }
 
 // ===========================================================================
@@ -1181,6 +1212,18 @@ static int glds_default_cfg(int Cin, int Cout, int ksize) {
 static int glds_cfg_tp(int cfg) {   // pixels per tile of a v2 config
   return (cfg == 21 || cfg == 22) ? 256 : (cfg == 23 || cfg == 25) ? 512 : 0;
 }
+// rows of the bias-partial matrix an LDS-DMA config writes: pixel tiles x waves along the pixels (0: none)
+static int glds_bpart_rows(int cfg, int M) {
+  int tp = 0, wp = 0;
+  switch (cfg) {
+    case 11: case 21: tp = 256; wp = 2; break;   // 256 ch x 256 px, 4 x 2 waves
+    case 12: case 22: tp = 256; wp = 4; break;   // 128 x 256, 2 x 4
+    case 13: case 23: tp = 512; wp = 8; break;   // 64 x 512, 1 x 8
+    case 25: tp = 512; wp = 4; break;            // 128 x 512, 2 x 4 (2 fragments per wave)
+    default: return 0;
+  }
+  return ((M + tp - 1) / tp) * wp;
+}
 
 template <int DT, int EPI>
 static int dispatch_glds(const ConvArgs2& a, int tile_cfg, hipStream_t s) {
@@ -1217,7 +1260,10 @@ static const bf16_t* conv_zero_page() {
 template <int DT>
 static int conv_igemm_impl(const void* x, const void* w, const float* bias, const void* mask, void* y,
                            int N, int H, int W, int Cin, int Cout, int ksize, int dil,
-                           int epi, int first, int tile_cfg, void* stream) {
+                           int epi, int first, int tile_cfg, void* stream, float* bpart, int bpart_cap,
+                           int* bpart_rows) {
+  if (bpart_rows) *bpart_rows = 0;
+  if (epi != EPI_MASK && epi != EPI_POOLBWD) bpart = nullptr;
   ConvArgs a;
   a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.bias = bias; a.mask = (const bf16_t*)mask;
   a.y = (bf16_t*)y; a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.ksize = ksize; a.dil = dil;
@@ -1252,6 +1298,11 @@ static int conv_igemm_impl(const void* x, const void* w, const float* bias, cons
     // Cout = 64: 64-column tiles, two blocks per CU (CANNET_HALO_TCOL128 = the 128-column tiles)
     const bool narrow = Cout == 64 && getenv("CANNET_HALO_TCOL128") == nullptr;
     h.N = N; h.H = H; h.W = W; h.tiles_x = narrow ? (W + 63) / 64 : (W + 127) / 128; h.tiles_y = (H + 3) / 4;
+    if (bpart != nullptr && epi == EPI_MASK) {
+      const int rows_per_tile = (Cout == 128) ? 4 : narrow ? 4 : 8;   // NW * 64 / CO
+      const long long rows = (long long)N * h.tiles_y * h.tiles_x * rows_per_tile;
+      if (rows <= bpart_cap) { h.bpart = bpart; if (bpart_rows) *bpart_rows = (int)rows; }
+    }
 #define CAN_HALO_CASE(E) \
     if (epi == E) return (Cout == 128) ? launch_halo64<DT, 128, E, 128>(h, s) \
                          : narrow ? launch_halo64<DT, 64, E, 64>(h, s) : launch_halo64<DT, 64, E, 128>(h, s);
@@ -1269,6 +1320,10 @@ static int conv_igemm_impl(const void* x, const void* w, const float* bias, cons
     if (!b.zero) return -10;
     if (epi == EPI_POOLBWD) { b.mask = nullptr; b.pcodes = (const uint32_t*)mask; }   // mask = max-pool codes
     b.H = H; b.W = W; b.Cin = Cin; b.Cout = Cout; b.ksize = ksize; b.dil = dil; b.M = a.M;
+    if (bpart != nullptr) {
+      const int rows = glds_bpart_rows(tile_cfg ? tile_cfg : glds_default_cfg(Cin, Cout, ksize), a.M);
+      if (rows > 0 && rows <= bpart_cap) { b.bpart = bpart; if (bpart_rows) *bpart_rows = rows; }
+    }
     b.fdW = make_fastdiv((uint32_t)W); b.fdH = make_fastdiv((uint32_t)H);
     switch (epi) {
       case EPI_BIAS_RELU: return dispatch_glds<DT, EPI_BIAS_RELU>(b, tile_cfg, s);
@@ -1340,11 +1395,14 @@ extern "C" int can_conv_f1(const void* x, const void* w, const float* bias, cons
 }
 
 // dt: element type of x / w / mask / y (DT_BF16 = 0, DT_F16 = 1)
+// bpart (optional, EPI_MASK / EPI_POOLBWD): fp32 [bpart_cap][Cout] buffer for the bias-gradient partials of the
+// produced gradient; *bpart_rows = rows written (0: this kernel path does not produce them)
 extern "C" int can_conv_igemm(const void* x, const void* w, const float* bias, const void* mask, void* y,
                               int N, int H, int W, int Cin, int Cout, int ksize, int dil,
-                              int epi, int first, int tile_cfg, int dt, void* stream) {
+                              int epi, int first, int tile_cfg, int dt, void* stream, float* bpart, int bpart_cap,
+                              int* bpart_rows) {
   CAN_DT_DISPATCH(dt, can::conv_igemm_impl<DT>(x, w, bias, mask, y, N, H, W, Cin, Cout, ksize, dil, epi, first,
-                                              tile_cfg, stream));
+                                              tile_cfg, stream, bpart, bpart_cap, bpart_rows));
 }
 
 extern "C" int can_conv_pool_fwd(const void* x, const void* w, const float* bias, void* y, void* yp, void* codes,

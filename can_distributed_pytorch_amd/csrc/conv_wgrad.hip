@@ -1218,6 +1218,34 @@ __global__ void __launch_bounds__(256) wgrad_reduce_tiled_kernel(const float* __
   }
 }
 
+// Bias partials produced by the data-gradient epilogue that wrote dY (conv_igemm.hip, EPI_MASK /
+// EPI_POOLBWD: one row per wave's pixel slice, up to ~10^5 rows): [R][C] -> [G][C], block g sums rows
+// [g*RPB, (g+1)*RPB) in order (deterministic), so the reduce kernels' bias blocks see <= 512 rows.
+__global__ void __launch_bounds__(256) bias_rows_reduce_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                               int R, int C, int RPB) {
+  __shared__ float4 red[256];
+  const int C4 = C >> 2;                       // C % 64 == 0, C <= 1024
+  const int groups = 256 / C4;
+  const int col = threadIdx.x % C4, rg = threadIdx.x / C4;
+  const int r0 = blockIdx.x * RPB, r1 = min(R, r0 + RPB);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (rg < groups) {
+    for (int r = r0 + rg; r < r1; r += groups) {
+      const float4 v = reinterpret_cast<const float4*>(in + (size_t)r * C)[col];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (rg == 0) {
+    for (int g = 1; g < groups; ++g) {
+      const float4 v = red[g * C4 + col];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    reinterpret_cast<float4*>(out + (size_t)blockIdx.x * C)[col] = acc;
+  }
+}
+
 static int launch_reduce2(const float* ws, const float* wsb, float* dw, float* db, int S, int Sb, int K, int Cout,
                           int Cin, int taps, int first, float beta, float scale, const float* dscale, hipStream_t s) {
   const size_t plane = (size_t)K * Cout;
@@ -1335,14 +1363,31 @@ static const can::bf16_t* zero_page() {
 template <int DT>
 static int conv_wgrad_impl(const void* dy, const void* x, float* ws, float* wsb, float* dw, float* db, int N, int H,
                            int W, int Cin, int Cout, int ksize, int dil, int first, int S, int mslice, int cfg,
-                           float beta, float scale, const float* dscale, void* stream) {
+                           float beta, float scale, const float* dscale, void* stream, const float* bext,
+                           int bext_rows) {
   using namespace can;
   hipStream_t s = (hipStream_t)stream;
   const int K = first ? 64 : ksize * ksize * Cin;
   if ((long long)K * Cout >= 0x7fffffffLL) return -9;   // 32-bit plane indexing in the reduction
-  float* wsb_used = (db != nullptr) ? wsb : nullptr;
+  // external bias partials (the dgrad epilogue that produced dY summed it): no bias work in the GEMM /
+  // column-sum kernels, only a rows pre-reduction into the workspace's bias area (<= kBiasParts rows)
+  const bool ext = (db != nullptr) && (bext != nullptr) && bext_rows > 0;
+  if (ext && (Cout % 64 || Cout > 1024)) return -15;
+  float* wsb_used = (db != nullptr && !ext) ? wsb : nullptr;
   int rc;
   int Sb = S;                       // bias partials summed by the reduce kernel
+  int Sb_ext = 0;
+  const float* bsrc = wsb;          // bias partial rows the reduce kernel sums (external: bext itself when short)
+  if (ext) {
+    if (bext_rows <= kBiasParts) {
+      bsrc = bext;
+      Sb_ext = bext_rows;
+    } else {
+      const int rpb = (bext_rows + kBiasParts - 1) / kBiasParts;
+      Sb_ext = (bext_rows + rpb - 1) / rpb;
+      hipLaunchKernelGGL(bias_rows_reduce_kernel, dim3(Sb_ext), dim3(256), 0, s, bext, wsb, bext_rows, Cout, rpb);
+    }
+  }
   if (first || cfg == 0) {
     if (Cin != 4 || Cout % 64) return -2;
     WgradArgs a;
@@ -1373,8 +1418,8 @@ static int conv_wgrad_impl(const void* dy, const void* x, float* ws, float* wsb,
       h.tiles_per_slice = (h.ntiles + S - 1) / S;
       rc = ring ? launch_halo_ring<DT, 64, 4>(h, s) : launch_halo<DT, 64, 2>(h, s);
       if (rc) return rc;
-      const int plane = K * Cout;
-      return launch_reduce2(ws, wsb_used, dw, db, S, S, K, Cout, Cin, 9, 0, beta, scale, dscale, s);
+      return ext ? launch_reduce2(ws, bsrc, dw, db, S, Sb_ext, K, Cout, Cin, 9, 0, beta, scale, dscale, s)
+                 : launch_reduce2(ws, wsb_used, dw, db, S, S, K, Cout, Cin, 9, 0, beta, scale, dscale, s);
     }
     switch (cfg) {
       case 1: if (Cout % 128) return -4; rc = launch_wgrad2<DT, 2, 2, 1, 4, 1, 2>(a, s); break;
@@ -1420,19 +1465,31 @@ static int conv_wgrad_impl(const void* dy, const void* x, float* ws, float* wsb,
     }
   }
   if (rc) return rc;
-  const int plane = K * Cout;
-  (void)plane;
+  if (ext) return launch_reduce2(ws, bsrc, dw, db, S, Sb_ext, K, Cout, first ? 4 : Cin, ksize * ksize, first, beta,
+                                 scale, dscale, s);
   return launch_reduce2(ws, wsb_used, dw, db, S, Sb, K, Cout, first ? 4 : Cin, ksize * ksize, first, beta, scale, dscale,
                         s);
 }
 
 // dt: element type of dy / x (DT_BF16 = 0, DT_F16 = 1); the gradients are fp32.  The result is
 // multiplied by scale and, when dscale is not null, by the device scalar dscale[0] (1 / loss scale).
+// bext (optional): [bext_rows][Cout] fp32 bias partials of dy already summed by its producer (the data-gradient
+// epilogue): db comes from them, the kernels here do no bias work
+extern "C" int can_bias_rows_reduce(const float* in, float* out, int R, int C, int rows_out, void* stream) {
+  if (C % 64 || C > 1024 || R < 1 || rows_out < 1) return -2;
+  const int rpb = (R + rows_out - 1) / rows_out;
+  const int g = (R + rpb - 1) / rpb;
+  hipLaunchKernelGGL(can::bias_rows_reduce_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, in, out, R, C, rpb);
+  if (hipGetLastError() != hipSuccess) return -3;
+  return g;                                   // rows written
+}
+
 extern "C" int can_conv_wgrad(const void* dy, const void* x, float* ws, float* wsb, float* dw, float* db, int N,
                               int H, int W, int Cin, int Cout, int ksize, int dil, int first, int S, int mslice,
-                              int cfg, float beta, float scale, const float* dscale, int dt, void* stream) {
+                              int cfg, float beta, float scale, const float* dscale, int dt, void* stream,
+                              const float* bext, int bext_rows) {
   CAN_DT_DISPATCH(dt, conv_wgrad_impl<DT>(dy, x, ws, wsb, dw, db, N, H, W, Cin, Cout, ksize, dil, first, S, mslice,
-                                          cfg, beta, scale, dscale, stream));
+                                          cfg, beta, scale, dscale, stream, bext, bext_rows));
 }
 
 // Batched 1x1 weight gradient without bias: nb problems dW_b[Cout][Cin] = sum_m dY_b[m][co] X_b[m][ci]

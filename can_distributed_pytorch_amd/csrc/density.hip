@@ -112,18 +112,28 @@ __global__ void __launch_bounds__(256) density_splat_kernel(const float2* __rest
   }
 }
 
+__global__ void density_fill_kernel(float* __restrict__ sigma, int n, float v) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) sigma[i] = v;
+}
+
 }  // namespace can
 
+// fixed_sigma > 0: every head gets that sigma (no kNN; the synthetic-data generator's fixed-width heads)
 extern "C" int can_density_map(const float* pts, int n, int H, int W, float* sigma_ws, float* out, int max_r,
-                               void* stream) {
+                               void* stream, float fixed_sigma) {
   using namespace can;
   hipStream_t s = (hipStream_t)stream;
   if (n <= 0) return 0;
   const size_t lds = (size_t)(H + W) * sizeof(float);
   if (lds > 150 * 1024) return -2;                      // weight tables of one clipped footprint in LDS
-  const float single = 0.25f * 0.5f * (float)(H + W);   // avg(shape)/2/2 (reference intent, Q9)
-  hipLaunchKernelGGL(density_knn_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const float2*)pts, n, sigma_ws,
-                     single);
+  if (fixed_sigma > 0.f) {
+    hipLaunchKernelGGL(density_fill_kernel, dim3((n + 255) / 256), dim3(256), 0, s, sigma_ws, n, fixed_sigma);
+  } else {
+    const float single = 0.25f * 0.5f * (float)(H + W);   // avg(shape)/2/2 (reference intent, Q9)
+    hipLaunchKernelGGL(density_knn_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const float2*)pts, n, sigma_ws,
+                       single);
+  }
   if (lds > 64 * 1024)
     CAN_HIP_CHECK(hipFuncSetAttribute((const void*)density_splat_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)lds));

@@ -75,6 +75,65 @@ def make_synthetic_batch(batch: int, h: int, w: int, seed: int = 0, device="cpu"
     return imgs.to(device), gts.to(device)
 
 
+def make_synthetic_batch_gpu(batch: int, h: int, w: int, seed: int = 0, device="cuda",
+                             heads: Tuple[int, int] = (100, 1500), dtype: torch.dtype = torch.bfloat16,
+                             nhwc4: bool = True, seeds=None):
+    """The same recipe rendered on the GPU (csrc/preprocess.hip synth_render + the density splat of
+    csrc/density.hip): only the head points and a coarse noise grid are drawn on the host.  Returns
+    (x4 [B,H,W,4] 16-bit NHWC4 — the first layer's input layout — or, nhwc4=False, img [B,3,H,W] fp32,
+    gt [B,1,H/8,W/8] fp32).  Statistically the CPU generator's images; not bitwise (different resampling
+    order).  seeds: optional per-image seeds (image i a function of seeds[i] alone: sharded datasets)."""
+    from ..ops import _ext
+    from ..ops.conv import dt_code
+    C = _ext.require()
+    assert h % 16 == 0 and w % 16 == 0, "H and W must be multiples of 16"
+    dev = torch.device(device)
+    gens = [torch.Generator().manual_seed(int(sd)) for sd in seeds] if seeds is not None else \
+        [torch.Generator().manual_seed(seed)] * batch
+    if len(gens) != batch:
+        raise ValueError("len(seeds) != batch")
+    pts, noise = [], torch.empty(batch, 3, h // 16, w // 16)
+    for b, gen in enumerate(gens):
+        n = int(torch.randint(heads[0], heads[1] + 1, (1,), generator=gen))
+        pts.append(synthetic_points(n, h, w, gen))
+        noise[b] = torch.rand(3, h // 16, w // 16, generator=gen)
+    dens = torch.zeros(batch, h, w, dtype=torch.float32, device=dev)
+    st = _ext.stream_ptr(dev)
+    for b, p in enumerate(pts):
+        pd = p.to(dev).contiguous()
+        sig = torch.empty(pd.shape[0], dtype=torch.float32, device=dev)
+        C.density_map(pd.data_ptr(), pd.shape[0], h, w, sig.data_ptr(), dens[b].data_ptr(), 0, st, 4.0)
+    x4 = torch.empty(batch, h, w, 4, dtype=dtype, device=dev)
+    gt = torch.empty(batch, 1, h // 8, w // 8, dtype=torch.float32, device=dev)
+    dmax = torch.empty(batch, dtype=torch.float32, device=dev)
+    nz = noise.to(dev)
+    C.synth_render(dens.data_ptr(), nz.data_ptr(), dmax.data_ptr(), x4.data_ptr(), gt.data_ptr(), batch, h, w,
+                   dt_code(dtype), st)
+    if nhwc4:
+        return x4, gt
+    return x4[..., :3].float().permute(0, 3, 1, 2).contiguous(), gt
+
+
+class SyntheticGPULoader:
+    """Batches of a synthetic crowd set rendered on the GPU, driven by a (distributed) batch sampler: image
+    ``index`` is a function of (seed, index) only, so ranks shard it exactly like a file dataset.  Yields
+    (x4 [B,H,W,4] NHWC4 16-bit, gt [B,1,H/8,W/8] fp32) already on ``device``."""
+
+    def __init__(self, batch_sampler, h: int, w: int, seed: int, device, dtype=torch.bfloat16,
+                 heads: Tuple[int, int] = (100, 1500)):
+        self.bs, self.h, self.w, self.seed = batch_sampler, h, w, seed
+        self.device, self.dtype, self.heads = device, dtype, heads
+
+    def __len__(self):
+        return len(self.bs)
+
+    def __iter__(self):
+        for idx in self.bs:
+            idx = [int(i[0]) if isinstance(i, (tuple, list)) else int(i) for i in idx]
+            yield make_synthetic_batch_gpu(len(idx), self.h, self.w, device=self.device, heads=self.heads,
+                                           dtype=self.dtype, seeds=[self.seed * 100003 + i for i in idx])
+
+
 def expected_flops_per_image(h: int, w: int) -> float:
     """Forward conv FLOPs (2*MAC) of CANNet at HxW input (733.4 GF at 768x1024)."""
     from ..models.cannet import FRONTEND_CFG, BACKEND_CFG
@@ -97,5 +156,5 @@ def expected_flops_per_image(h: int, w: int) -> float:
     return fl
 
 
-__all__ = ["make_synthetic_batch", "synthetic_points", "density_from_points_fixed",
+__all__ = ["make_synthetic_batch", "make_synthetic_batch_gpu", "SyntheticGPULoader", "synthetic_points", "density_from_points_fixed",
            "expected_flops_per_image", "IMAGENET_MEAN", "IMAGENET_STD", "math"]

@@ -75,12 +75,15 @@ def _check_act(x: torch.Tensor, name: str, c: Optional[int] = None, dtype: Optio
 
 def conv_igemm(x: torch.Tensor, wpack: torch.Tensor, bias: Optional[torch.Tensor], *, ksize: int, dil: int = 1,
                epi: int = EPI_BIAS_RELU, mask: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-               first: bool = False, tile: int = 0) -> torch.Tensor:
+               first: bool = False, tile: int = 0, bias_part: Optional[torch.Tensor] = None):
     """y[N,H,W,Co] = epi(conv(x[N,H,W,Ci], W) ...), stride 1, 'same' padding = dil*(ksize//2).
 
     epi=EPI_POOLBWD: the conv result is d(maxpool output); ``mask`` is the pool's max-pool codes
     (int32 [N,H,W,Co/8], see ``maxpool_codes``) and the result is written as d(pool input) (ReLU mask of the
-    pool input included) into [N,2H,2W,Co]."""
+    pool input included) into [N,2H,2W,Co].
+
+    bias_part (EPI_MASK / EPI_POOLBWD): fp32 [cap, Co] buffer; the epilogue writes the bias-gradient partials
+    of its output into its first rows and (out, bias_part[:rows] or None) is returned instead of out."""
     C = _ext.require()
     if x.dim() != 4:
         raise ValueError("x must be [N,H,W,C]")
@@ -122,10 +125,51 @@ def conv_igemm(x: torch.Tensor, wpack: torch.Tensor, bias: Optional[torch.Tensor
         _check_act(out, "out", dtype=dt)
     if n * h * w >= 2 ** 31 // max(ci, co):
         raise ValueError("tensor too large for 32-bit pixel indexing")
-    C.conv_igemm(x.data_ptr(), wpack.data_ptr(), bias.data_ptr() if bias is not None else 0,
-                 mask.data_ptr() if mask is not None else 0, out.data_ptr(), n, h, w, ci, co, ksize, dil,
-                 epi, int(first), tile, dt_code(dt), _ext.stream_ptr(x.device))
+    bp_ptr, bp_cap = 0, 0
+    if bias_part is not None:
+        if epi not in (EPI_MASK, EPI_POOLBWD):
+            raise ValueError("bias partials come from data-gradient epilogues (EPI_MASK / EPI_POOLBWD)")
+        if bias_part.dtype != torch.float32 or not bias_part.is_contiguous() or bias_part.dim() != 2 or \
+                bias_part.shape[1] != co:
+            raise ValueError(f"bias_part must be a contiguous fp32 [rows, {co}] tensor")
+        bp_ptr, bp_cap = bias_part.data_ptr(), bias_part.shape[0]
+    rows = C.conv_igemm(x.data_ptr(), wpack.data_ptr(), bias.data_ptr() if bias is not None else 0,
+                        mask.data_ptr() if mask is not None else 0, out.data_ptr(), n, h, w, ci, co, ksize, dil,
+                        epi, int(first), tile, dt_code(dt), _ext.stream_ptr(x.device), bp_ptr, bp_cap)
+    if bias_part is not None:
+        return out, (bias_part[:rows] if rows > 0 else None)
     return out
+
+
+BIAS_ROWS = 512     # bias partial rows the weight-gradient reduce kernels take directly (kBiasParts)
+
+
+def bias_part_capacity(n: int, h: int, w: int) -> int:
+    """Rows a data-gradient epilogue may write for an output of n x h x w pixels (pooled resolution for
+    EPI_POOLBWD): LDS-DMA kernels one row per (pixel tile, wave slot) = ceil(M / 64) at most, the halo
+    kernel one per (4 x 64 tile, wave slot)."""
+    return max(-(-n * h * w // 64) + 64, n * (-(-h // 4)) * (-(-w // 64)) * 8)
+
+
+def conv_dgrad_with_bias(dy: torch.Tensor, wpack: torch.Tensor, *, ksize: int, dil: int = 1, epi: int = EPI_MASK,
+                         mask: torch.Tensor, tile: int = 0):
+    """Data gradient (EPI_MASK / EPI_POOLBWD) whose epilogue also sums the bias gradient of the gradient it
+    writes (the next layer's dY): returns (dX, partials [rows, Cin] fp32 or None when the kernel path does not
+    produce them).  conv_wgrad(bias_partials=...) reduces them into db instead of re-reading dY."""
+    n, h, w, _ = dy.shape
+    co = wpack.shape[0]
+    bp = torch.empty(bias_part_capacity(n, h, w), co, dtype=torch.float32, device=dy.device)
+    out, part = conv_igemm(dy, wpack, None, ksize=ksize, dil=dil, epi=epi, mask=mask, tile=tile, bias_part=bp)
+    if part is not None and part.shape[0] > BIAS_ROWS:
+        # long partial lists (the halo kernel: one row per 4 x 64 tile slot) are folded right here, on the
+        # producer's stream where the CUs the dgrad just released are free; a short launch queued on the
+        # weight-gradient stream would wait for CUs behind the next data-gradient kernel
+        C = _ext.require()
+        red = torch.empty(BIAS_ROWS, co, dtype=torch.float32, device=dy.device)
+        g = C.bias_rows_reduce(part.data_ptr(), red.data_ptr(), part.shape[0], co, BIAS_ROWS,
+                               _ext.stream_ptr(dy.device))
+        part = red[:g]
+    return out, part
 
 
 def _check_codes(codes: Optional[torch.Tensor], pooled_shape) -> None:
@@ -190,9 +234,12 @@ class WgradWorkspace:
 
 def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, db: Optional[torch.Tensor], *, ksize: int,
                dil: int = 1, first: bool = False, ws: Optional[WgradWorkspace] = None, beta: float = 0.0,
-               scale: float = 1.0, dscale: Optional[torch.Tensor] = None) -> None:
+               scale: float = 1.0, dscale: Optional[torch.Tensor] = None,
+               bias_partials: Optional[torch.Tensor] = None) -> None:
     """dw[Co,Ci,kh,kw] (fp32, PyTorch layout) = scale * [dscale[0]] * sum_m dY[m,co] Xcol[m,k] (+ beta*dw);
-    db likewise.  dscale: optional fp32 device scalar read at run time (1 / loss scale of the fp16 step)."""
+    db likewise.  dscale: optional fp32 device scalar read at run time (1 / loss scale of the fp16 step).
+    bias_partials: [rows, Co] fp32 per-slice sums of dY written by the data-gradient epilogue that produced it
+    (conv_dgrad_with_bias): db is reduced from them and dY is not re-read for the bias."""
     C = _ext.require()
     _check_act(dy, "dy")
     _check_act(x, "x", dtype=dy.dtype)
@@ -219,10 +266,16 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, db: Optional
     buf = ws.reserve(need)
     ktot = 64 if first else ksize * ksize * ci
     wsb_ptr = buf.data_ptr() + 4 * s * ktot * co
+    bx, brows = 0, 0
+    if bias_partials is not None and db is not None:
+        if bias_partials.dtype != torch.float32 or not bias_partials.is_contiguous() or bias_partials.dim() != 2 or \
+                bias_partials.shape[1] != co or co > 1024:
+            raise ValueError(f"bias_partials must be a contiguous fp32 [rows, {co}] tensor (Cout <= 1024)")
+        bx, brows = bias_partials.data_ptr(), bias_partials.shape[0]
     C.conv_wgrad(dy.data_ptr(), x.data_ptr(), buf.data_ptr(), wsb_ptr, dw.data_ptr(),
                  db.data_ptr() if db is not None else 0, n, h, w, ci, co, ksize, dil, int(first), s, mslice, cfg,
                  float(beta), float(scale), dscale.data_ptr() if dscale is not None else 0, dt_code(dy.dtype),
-                 _ext.stream_ptr(x.device))
+                 _ext.stream_ptr(x.device), bx, brows)
 
 
 def wgrad_1x1_batched_plan(m: int, nb: int, ci: int, co: int, ncu: int = 256):

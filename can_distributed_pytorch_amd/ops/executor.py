@@ -335,26 +335,41 @@ class CANNetExecutor:
         side = self._side_stream()
         hold = []          # operands of side-stream work, kept alive until the join below
 
-        def wg(spec_or_w, dy, x, ksize, dil, first, wi, bi):
+        # CANNET_BIAS_FUSED=1: the data-gradient epilogues also sum the bias gradient of the dY they write, so
+        # the weight-gradient launch need not re-read dY for db.  Off by default: measured 421-423 vs 427 img/s
+        # (profiles/r2/README.md) — folding the ~10^4 - 10^5 partial rows needs a short extra launch, and any
+        # short launch waits for CUs behind the one-block-per-CU GEMMs of the other stream (50-100 us each)
+        fuse_bias = os.environ.get("CANNET_BIAS_FUSED", "0") == "1"
+
+        def wg(spec_or_w, dy, x, ksize, dil, first, wi, bi, bp=None):
+            # bp: bias partials of dy summed by the data-gradient epilogue that wrote it (None: the weight-
+            # gradient launch re-reads dy for the bias)
             def run():
                 C.conv_wgrad(dy, x, grads[wi], grads[bi] if bi is not None else None, ksize=ksize, dil=dil,
-                             first=first, ws=ws, beta=beta, scale=scale, dscale=dscale)
+                             first=first, ws=ws, beta=beta, scale=scale, dscale=dscale, bias_partials=bp)
                 ready([wi] + ([bi] if bi is not None else []))
-            self._on_side(side, run, hold, dy, x)
+            self._on_side(side, run, hold, dy, x, *(() if bp is None else (bp,)))
+
+        def dgrad(dy, dgr, dil, epi, mask):
+            """Data gradient; returns (dX, bias partials of dX or None)."""
+            if fuse_bias:
+                return C.conv_dgrad_with_bias(dy, dgr, ksize=3, dil=dil, epi=epi, mask=mask)
+            return C.conv_igemm(dy, dgr, None, ksize=3, dil=dil, epi=epi, mask=mask), None
 
         # ---- backend, reverse
-        dy = d_b6
+        dy, bp = d_b6, None
         for s in reversed(self.back):
             x = sv["back_in"][s.idx]
-            wg(s, dy, x, 3, s.dil, False, s.w_index, s.b_index)
+            wg(s, dy, x, 3, s.dil, False, s.w_index, s.b_index, bp)
             _, dgr = self.packs[id(s.module.weight)]
             if s.idx > 0:
-                dy = C.conv_igemm(dy, dgr, None, ksize=3, dil=s.dil, epi=C.EPI_MASK, mask=x)
+                dy, bp = dgrad(dy, dgr, s.dil, C.EPI_MASK, x)
             else:
                 dcat = C.conv_igemm(dy, dgr, None, ksize=3, dil=s.dil, epi=C.EPI_NONE)
         # ---- context module
         dy = self._context_bwd(sv["ctx"], sv["fv"], dcat, grads, ws, beta, scale, ready, dscale, side, hold)
         # ---- frontend, reverse
+        bp = None
         for s in reversed(self.front):
             x = sv["front_in"][s.idx]
             if sv.get("f1") and s.idx == 1:
@@ -368,9 +383,9 @@ class CANNetExecutor:
                                     scale=scale, dscale=dscale)
                     ready([s.w_index, s.b_index])
                 self._on_side(side, run_f1, hold, dy2, x)
-                dy = C.conv_f1(dy, dgr, None, x, w1, b1, epi=C.EPI_MASK)
+                dy, bp = C.conv_f1(dy, dgr, None, x, w1, b1, epi=C.EPI_MASK), None
                 continue
-            wg(s, dy, x, 3, 1, s.first, s.w_index, s.b_index)
+            wg(s, dy, x, 3, 1, s.first, s.w_index, s.b_index, bp)
             if s.idx == 0:
                 break
             _, dgr = self.packs[id(s.module.weight)]
@@ -381,12 +396,12 @@ class CANNetExecutor:
                 # round-trips through memory
                 codes = sv["pre_pool"][prev.idx]
                 if os.environ.get("CANNET_POOLBWD_FUSED", "1") != "0":
-                    dy = C.conv_igemm(dy, dgr, None, ksize=3, dil=1, epi=C.EPI_POOLBWD, mask=codes)
+                    dy, bp = dgrad(dy, dgr, 1, C.EPI_POOLBWD, codes)
                 else:
                     dp = C.conv_igemm(dy, dgr, None, ksize=3, dil=1, epi=C.EPI_NONE)
-                    dy = C.maxpool_bwd_codes(codes, dp)
+                    dy, bp = C.maxpool_bwd_codes(codes, dp), None
             else:
-                dy = C.conv_igemm(dy, dgr, None, ksize=3, dil=1, epi=C.EPI_MASK, mask=x)
+                dy, bp = dgrad(dy, dgr, 1, C.EPI_MASK, x)
         if side is not None:
             torch.cuda.current_stream(d_b6.device).wait_stream(side)     # join: every gradient written
         hold.clear()

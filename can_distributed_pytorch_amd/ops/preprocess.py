@@ -3,6 +3,12 @@
 Same result as CrowdDataset's CPU transform (data/transforms.py:prepare_pair,
 reference model/CrowdDataset.py:38-67) but computed by csrc/preprocess.hip
 on the GPU, writing the first conv layer's NHWC4 bf16 layout directly.
+
+Per batch: the DataLoader worker packs the decoded samples back to back
+(``PackedCollate``: one uint8 image buffer, one fp32 density buffer, a
+descriptor table), the main process makes one pinned H2D copy of each and
+ONE kernel launch turns the batch into network inputs (``preprocess_packed``).
+``preprocess_batch`` is the per-sample form (tests / variable-size use).
 """
 from __future__ import annotations
 
@@ -52,3 +58,53 @@ class RawCollate:
     def __call__(self, batch: List):
         imgs, dens, flips = zip(*batch)
         return list(imgs), list(dens), list(flips)
+
+
+class PackedCollate:
+    """collate_fn for CrowdDataset(raw=True) that packs a batch for ONE H2D copy per buffer and ONE launch:
+    returns (images uint8 [sum of H*W*C], densities fp32 [sum of H*W], desc int64 [n, 8], (Ho, Wo)) with
+    desc[i] = (image byte offset, H0, W0, C, flip, density offset, 0, 0).  Runs in the loader workers, so the
+    main process only copies; pin_memory=True pins the two big buffers."""
+
+    def __init__(self, downsample: int = 8):
+        self.ds = downsample
+
+    def __call__(self, batch: List):
+        imgs, dens, flips = zip(*batch)
+        h0, w0 = imgs[0].shape[:2]
+        ho, wo = (h0 // self.ds) * self.ds, (w0 // self.ds) * self.ds
+        desc = torch.zeros(len(imgs), 8, dtype=torch.int64)
+        ioff = doff = 0
+        for i, (im, dm, fl) in enumerate(zip(imgs, dens, flips)):
+            hh, ww = im.shape[:2]
+            if (hh // self.ds * self.ds, ww // self.ds * self.ds) != (ho, wo):
+                raise ValueError("all samples of a batch must resize to the same shape")
+            if tuple(dm.shape) != (hh, ww):
+                raise ValueError("density must match the image size")
+            ch = 1 if im.dim() == 2 else im.shape[2]
+            desc[i] = torch.tensor([ioff, hh, ww, ch, int(bool(fl)), doff, 0, 0])
+            ioff += hh * ww * ch
+            doff += hh * ww
+        ibuf = torch.cat([im.reshape(-1) for im in imgs])
+        dbuf = torch.cat([dm.reshape(-1).float() for dm in dens])
+        return ibuf, dbuf, desc, (ho, wo)
+
+
+def preprocess_packed(packed, device, downsample: int = 8, dtype: torch.dtype = torch.bfloat16):
+    """PackedCollate output -> (x4 [N,Ho,Wo,4] 16-bit NHWC4, gt [N,1,Ho/d,Wo/d] fp32): one copy per buffer, one
+    launch for the whole batch (images and densities)."""
+    C = _ext.require()
+    ibuf, dbuf, desc, (ho, wo) = packed
+    if ibuf.dtype != torch.uint8 or dbuf.dtype != torch.float32 or desc.dtype != torch.int64:
+        raise ValueError("packed batch: uint8 images, fp32 densities, int64 descriptors")
+    dev = torch.device(device)
+    n = desc.shape[0]
+    from .conv import dt_code
+    ib = ibuf.to(dev, non_blocking=True)
+    db = dbuf.to(dev, non_blocking=True)
+    ds = desc.to(dev, non_blocking=True)
+    x4 = torch.empty(n, ho, wo, 4, dtype=dtype, device=dev)
+    gt = torch.empty(n, 1, ho // downsample, wo // downsample, dtype=torch.float32, device=dev)
+    C.preprocess_batch(ib.data_ptr(), db.data_ptr(), ds.data_ptr(), n, x4.data_ptr(), gt.data_ptr(), ho, wo,
+                       downsample, dt_code(dtype), _ext.stream_ptr(dev))
+    return x4, gt

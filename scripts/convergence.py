@@ -1,0 +1,119 @@
+#!/usr/bin/env python
+"""Training-curve parity: native bf16 step (HIP kernels, fused SGD) vs the stock fp32 PyTorch step
+(nn.Conv2d / MIOpen, torch.optim.SGD) — the reference's numerics (train.py:126, no autocast) — from ONE
+initialisation, on one fixed synthetic crowd set.
+
+Per epoch and implementation: mean training loss (MSE sum, utils/train_eval_utils.py:20,37) and the
+count MAE on a held-out synthetic set (utils/train_eval_utils.py:83: |sum(et) - sum(gt)| per image).
+Both runs see the same batches in the same order.  Weights use He init (the reference's random
+normal(0.01) init starts from a vanishing signal and only trains from VGG-16 weights, which cannot be
+downloaded here).  Writes one JSON line per (impl, epoch) to --out and a summary line at the end.
+
+usage: python scripts/convergence.py --epochs 40 --out profiles/r2_convergence/curves.jsonl
+"""
+import argparse
+import copy
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from can_distributed_pytorch_amd.data.synthetic import make_synthetic_batch  # noqa: E402
+from can_distributed_pytorch_amd.models import CANNet  # noqa: E402
+
+
+def he_init(model, seed):
+    torch.manual_seed(seed)
+    for m in model.modules():
+        if isinstance(m, torch.nn.Conv2d):
+            fan_in = m.in_channels * m.kernel_size[0] * m.kernel_size[1]
+            torch.nn.init.normal_(m.weight, std=(2.0 / fan_in) ** 0.5)
+            if m.bias is not None:
+                torch.nn.init.zeros_(m.bias)
+    return model
+
+
+@torch.no_grad()
+def count_mae(model, test):
+    model.eval()
+    err = 0.0
+    for img, gt in test:
+        et = model(img)
+        err += (et.flatten(1).sum(1) - gt.flatten(1).sum(1)).abs().sum().item()
+    model.train()
+    return err / sum(img.shape[0] for img, _ in test)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--epochs", type=int, default=40)
+    ap.add_argument("--train", type=int, default=64, help="training images")
+    ap.add_argument("--test", type=int, default=16)
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--height", type=int, default=256)
+    ap.add_argument("--width", type=int, default=384)
+    ap.add_argument("--lr", type=float, default=2e-7)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--out", default="gpurun_out/convergence.jsonl")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    h, w, b = a.height, a.width, a.batch
+    train = [make_synthetic_batch(b, h, w, seed=10_000 + i, device=dev, heads=(20, 400)) for i in range(a.train // b)]
+    test = [make_synthetic_batch(b, h, w, seed=20_000 + i, device=dev, heads=(20, 400)) for i in range(a.test // b)]
+    base = he_init(CANNet(backend="torch"), a.seed)
+    os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
+    out = open(a.out, "w")
+    curves = {}
+    from can_distributed_pytorch_amd.engine.native import NativeStepper
+    from can_distributed_pytorch_amd.engine.trainer import TorchStepper
+    for impl in ("torch_fp32", "native_bf16"):
+        model = copy.deepcopy(base)
+        if impl == "torch_fp32":
+            st = TorchStepper(dev, dtype="fp32", lr=a.lr, model=model)
+            net = st.model
+        else:
+            model.exec_backend = "hip"
+            st = NativeStepper(dev, dtype="bf16", lr=a.lr, graph=False, model=model)
+            net = st.model
+        rows = []
+        mae0 = count_mae(net, test)
+        rows.append({"impl": impl, "epoch": -1, "train_loss": None, "test_mae": mae0})
+        out.write(json.dumps(rows[-1]) + "\n")
+        order = torch.Generator().manual_seed(a.seed)
+        t0 = time.time()
+        for ep in range(a.epochs):
+            perm = torch.randperm(len(train), generator=order).tolist()
+            tot = torch.zeros((), device=dev)
+            for i in perm:
+                tot += st.step(*train[i]).reshape(())
+            loss = float(tot) / len(perm)
+            mae = count_mae(net, test)
+            rows.append({"impl": impl, "epoch": ep, "train_loss": loss, "test_mae": mae,
+                         "steps": (ep + 1) * len(perm), "wall_s": round(time.time() - t0, 2)})
+            out.write(json.dumps(rows[-1]) + "\n")
+            out.flush()
+            print(json.dumps(rows[-1]), flush=True)
+        curves[impl] = rows
+    # summary: per-epoch relative gaps of the native curve to the fp32 one
+    tl = [(r["train_loss"], q["train_loss"]) for r, q in zip(curves["torch_fp32"][1:], curves["native_bf16"][1:])]
+    tm = [(r["test_mae"], q["test_mae"]) for r, q in zip(curves["torch_fp32"], curves["native_bf16"])]
+    summ = {
+        "summary": True, "epochs": a.epochs, "steps": a.epochs * (a.train // b), "image_hw": [h, w], "batch": b,
+        "lr": a.lr,
+        "fp32_loss_first_last": [tl[0][0], tl[-1][0]], "native_loss_first_last": [tl[0][1], tl[-1][1]],
+        "fp32_mae_init_last": [tm[0][0], tm[-1][0]], "native_mae_init_last": [tm[0][1], tm[-1][1]],
+        "max_rel_loss_gap": max(abs(q - r) / abs(r) for r, q in tl),
+        "max_abs_mae_gap": max(abs(q - r) for r, q in tm),
+        "mae_gap_last": tm[-1][1] - tm[-1][0],
+    }
+    out.write(json.dumps(summ) + "\n")
+    print(json.dumps(summ), flush=True)
+
+
+if __name__ == "__main__":
+    main()

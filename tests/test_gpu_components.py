@@ -202,6 +202,47 @@ def test_no_uninitialized_reads_poisoned_allocator():
     assert torch.equal(outs[0], outs[1])
 
 
+def test_packed_batch_preprocess_matches_cpu_transform():
+    """PackedCollate (in the loader workers) + preprocess_packed (one H2D copy per buffer, ONE launch for the
+    batch) == data/transforms.prepare_pair per sample (cv2 INTER_LINEAR semantics), incl. flips, mixed source
+    sizes that resize to one shape, gray images."""
+    import numpy as np
+    from can_distributed_pytorch_amd.data.transforms import prepare_pair
+    from can_distributed_pytorch_amd.ops.preprocess import PackedCollate, preprocess_packed
+    rng = np.random.default_rng(9)
+    shapes = [(77, 101, 3), (72, 96, 3), (79, 103, 1), (72, 100, 3)]        # all -> 72 x 96
+    samples, refs = [], []
+    for i, (h, w, c) in enumerate(shapes):
+        img = (rng.random((h, w, c) if c > 1 else (h, w)) * 255).astype(np.uint8)
+        dm = rng.random((h, w)).astype(np.float32)
+        flip = bool(i % 2)
+        samples.append((torch.from_numpy(img), torch.from_numpy(dm), flip))
+        refs.append(prepare_pair(img, dm, 8, flip))
+    packed = PackedCollate()(samples)
+    x4, gt = preprocess_packed(packed, "cuda")
+    assert tuple(x4.shape) == (4, 72, 96, 4) and tuple(gt.shape) == (4, 1, 9, 12)
+    for i, (ri, rg) in enumerate(refs):
+        got = x4[i, ..., :3].float().permute(2, 0, 1).cpu().numpy()
+        assert np.abs(got - ri).max() < 0.03
+        assert np.abs(gt[i].cpu().numpy() - rg).max() < 1e-3
+    assert bool((x4[..., 3] == 0).all())
+
+
+def test_synthetic_gpu_generator():
+    """GPU-rendered synthetic crowds: count-preserving ground truth (sum = number of heads inside, up to the
+    border mass), deterministic per seed, NHWC4 with channel 3 zero, statistics of the CPU recipe."""
+    from can_distributed_pytorch_amd.data.synthetic import make_synthetic_batch, make_synthetic_batch_gpu
+    x4, gt = make_synthetic_batch_gpu(2, 128, 192, seeds=[5, 6], heads=(50, 60))
+    x4b, gtb = make_synthetic_batch_gpu(2, 128, 192, seeds=[5, 6], heads=(50, 60))
+    torch.cuda.synchronize()
+    assert torch.equal(x4, x4b) and torch.equal(gt, gtb)
+    assert bool((x4[..., 3] == 0).all())
+    counts = gt.flatten(1).sum(1)
+    assert bool(((counts > 40) & (counts < 61)).all()), counts
+    img_cpu, gt_cpu = make_synthetic_batch(2, 128, 192, seed=5, heads=(50, 60))
+    assert abs(float(x4[..., :3].float().mean()) - float(img_cpu.mean())) < 0.5
+
+
 def test_gpu_preprocess_matches_cpu_transform():
     """ops/preprocess (HIP) == data/transforms.prepare_pair (cv2 INTER_LINEAR semantics), incl. flip."""
     import numpy as np

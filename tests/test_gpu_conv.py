@@ -327,3 +327,44 @@ def test_conv1_2_with_conv1_1_recomputed_is_bitwise_stored_path(n, h, w, dtype, 
     else:
         _close(dw, dw_ref, 1e-3)
         _close(db, db_ref, 1e-3)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("n,h,w,ci,co,dil,epi", [
+    (2, 12, 20, 128, 64, 1, "pool"), (1, 9, 13, 256, 128, 1, "pool"), (2, 6, 64, 512, 256, 1, "pool"),
+    (2, 16, 96, 64, 64, 1, "mask"), (1, 10, 70, 128, 64, 1, "mask"), (2, 12, 128, 128, 128, 1, "mask"),
+    (2, 8, 64, 512, 512, 2, "mask"), (1, 5, 40, 256, 128, 2, "mask"), (2, 8, 128, 64, 128, 1, "mask")])
+def test_dgrad_bias_partials_feed_wgrad(n, h, w, ci, co, dil, epi, dtype):
+    """The data-gradient epilogue's bias partials (EPI_MASK on the LDS-DMA and halo kernels, EPI_POOLBWD through
+    the max-pool codes) reduce to the bias gradient of the tensor it writes: db from the partials == db from
+    re-reading dY (bias_colsum / in-GEMM), and dW is untouched by the switch.  Here the conv maps co -> ci
+    (dgrad of a ci -> co layer), so dX has ci channels."""
+    from can_distributed_pytorch_amd.ops import conv as C
+    torch.manual_seed(21)
+    wt = (torch.randn(co, ci, 3, 3, device="cuda") * 0.05).to(dtype).float()   # layer ci -> co
+    pack = C.pack_weight_dgrad(wt, dtype)                                         # dgrad: co -> ci
+    dy = torch.randn(n, h, w, co, device="cuda").to(dtype)
+    if epi == "pool":
+        full = torch.relu(torch.randn(n, 2 * h, 2 * w, ci, device="cuda")).to(dtype)
+        _, mask = C.maxpool_codes(full)
+        e = C.EPI_POOLBWD
+    else:
+        mask = torch.randn(n, h, w, ci, device="cuda").to(dtype)
+        e = C.EPI_MASK
+    dx, bp = C.conv_dgrad_with_bias(dy, pack, ksize=3, dil=dil, epi=e, mask=mask)
+    dx_plain = C.conv_igemm(dy, pack, None, ksize=3, dil=dil, epi=e, mask=mask)
+    assert bp is not None and bp.shape[1] == ci
+    torch.cuda.synchronize()
+    assert torch.equal(dx, dx_plain)                       # the partials do not change the written gradient
+    # dX is the dY of the previous layer (ci channels): its weight gradient against some input
+    xin = torch.randn(*dx.shape[:3], 64, device="cuda").to(dtype)
+    dw1, db1 = torch.empty(ci, 64, 3, 3, device="cuda"), torch.empty(ci, device="cuda")
+    dw2, db2 = torch.empty_like(dw1), torch.empty_like(db1)
+    C.conv_wgrad(dx, xin, dw1, db1, ksize=3)
+    C.conv_wgrad(dx, xin, dw2, db2, ksize=3, bias_partials=bp)
+    torch.cuda.synchronize()
+    assert torch.equal(dw1, dw2)
+    ref = dx.float().sum(dim=(0, 1, 2))
+    # partials sum the unrounded fp32 values: equal to the rounded-dY column sums to rounding
+    assert torch.allclose(db2, ref, rtol=2e-2, atol=2e-2 * ref.abs().mean().item())
+    assert torch.allclose(db1, ref, rtol=1e-3, atol=1e-3)

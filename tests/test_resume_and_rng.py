@@ -33,11 +33,16 @@ def _batch(step):
 
 
 def test_resume_is_bitwise_exact(tmp_path):
-    # oneDNN may pick a different conv algorithm on a model's first call than on later ones (measured: the
-    # uninterrupted run's 4th step and a freshly loaded model's 1st step differed in the last bits), so the
-    # comparison runs on ATen's native CPU convolution, which is deterministic call to call
-    with torch.backends.mkldnn.flags(enabled=False):
-        _resume_case(tmp_path)
+    # oneDNN may pick a different conv algorithm on a model's first call than on later ones, and multithreaded
+    # CPU reductions change the summation order run to run (measured: the last bits of some gradients
+    # differed), so the comparison runs on ATen's native CPU convolution with one thread: deterministic
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        with torch.backends.mkldnn.flags(enabled=False):
+            _resume_case(tmp_path)
+    finally:
+        torch.set_num_threads(nt)
 
 
 def _resume_case(tmp_path):

@@ -72,7 +72,7 @@ def build_parser():
                         "weight gradients on a side stream, which the ROCm graph serialises)")
     p.add_argument("--bucket-mb", type=float, default=25.0)
     p.add_argument("--seed", type=int, default=0)
-    p.add_argument("--num-workers", type=int, default=4)
+    p.add_argument("--num-workers", type=int, default=8, help="JPEG-decoding DataLoader workers per rank")
     p.add_argument("--lr-schedule", choices=["none", "cosine"], default="none")
     p.add_argument("--checkpoint-dir", default="checkpoints")
     p.add_argument("--resume", type=str, default="", help="resume from a last_state.pth written by this script")
@@ -87,11 +87,15 @@ def build_parser():
     return p
 
 
-def make_loaders(args, world, rank, raw=False):
+def make_loaders(args, world, rank, raw=False, device=None, dtype=None):
+    """Train / test loaders.  raw=True: decoded uint8 samples packed per batch in the workers (PackedCollate),
+    one H2D copy + one preprocessing launch per batch on the GPU.  Synthetic data on a GPU run is rendered on
+    the GPU (SyntheticGPULoader), sharded by the same DistributedSampler."""
     from torch.utils.data import DataLoader, DistributedSampler, BatchSampler
     from can_distributed_pytorch_amd.data import CrowdDataset, SyntheticCrowdDataset
-    from can_distributed_pytorch_amd.ops.preprocess import RawCollate
-    collate = RawCollate() if raw else None
+    from can_distributed_pytorch_amd.data.dataset import EpochTaggedSampler
+    from can_distributed_pytorch_amd.ops.preprocess import PackedCollate
+    collate = PackedCollate() if raw else None
     if args.synthetic:
         h, w = (int(v) for v in args.synthetic.lower().split("x"))
         train_ds = SyntheticCrowdDataset(args.synthetic_n, h, w, seed=args.seed)
@@ -102,14 +106,21 @@ def make_loaders(args, world, rank, raw=False):
                                 gt_downsample=8, phase="train", seed=args.seed, raw=raw)
         test_ds = CrowdDataset(os.path.join(r, "test_data", "images"), os.path.join(r, "test_data", "ground_truth"),
                                gt_downsample=8, phase="test", raw=raw)
-    from can_distributed_pytorch_amd.data.dataset import EpochTaggedSampler
     train_sampler = DistributedSampler(train_ds, num_replicas=world, rank=rank, shuffle=True, seed=args.seed)
     test_sampler = DistributedSampler(test_ds, num_replicas=world, rank=rank, shuffle=True, seed=args.seed)
     # indices carry the epoch into (persistent) workers: the flip is a function of (seed, epoch, index)
     bs = BatchSampler(EpochTaggedSampler(train_sampler), args.batch_size, drop_last=False)
+    if args.synthetic and device is not None and device.type == "cuda" and args.impl == "hip" and \
+            h % 16 == 0 and w % 16 == 0:
+        from can_distributed_pytorch_amd.data.synthetic import SyntheticGPULoader
+        train_loader = SyntheticGPULoader(bs, h, w, args.seed, device, dtype=dtype)
+        test_loader = SyntheticGPULoader(BatchSampler(test_sampler, args.batch_size, drop_last=False), h, w,
+                                         args.seed + 1, device, dtype=dtype)
+        return train_loader, test_loader, train_sampler, test_sampler
     pin = torch.cuda.is_available()
     train_loader = DataLoader(train_ds, batch_sampler=bs, num_workers=args.num_workers, pin_memory=pin,
-                              persistent_workers=args.num_workers > 0, collate_fn=collate)
+                              persistent_workers=args.num_workers > 0, collate_fn=collate,
+                              prefetch_factor=4 if args.num_workers > 0 else None)
     test_loader = DataLoader(test_ds, sampler=test_sampler, batch_size=args.batch_size, num_workers=args.num_workers,
                              pin_memory=pin, shuffle=False, collate_fn=collate)
     return train_loader, test_loader, train_sampler, test_sampler
@@ -138,12 +149,13 @@ def main(args):
         print(f"[train start {time.strftime('%Y.%m.%d %H:%M:%S')}] world {world} impl {args.impl} {args}")
 
     raw = bool(args.gpu_preprocess and args.impl == "hip" and not args.synthetic)
-    train_loader, test_loader, train_sampler, test_sampler = make_loaders(args, world, rank, raw=raw)
+    act = torch.float16 if args.dtype == "fp16" else torch.bfloat16
+    train_loader, test_loader, train_sampler, test_sampler = make_loaders(args, world, rank, raw=raw, device=device,
+                                                                          dtype=act)
     prep = None
     if raw:
-        from can_distributed_pytorch_amd.ops.preprocess import preprocess_batch
-        act = torch.float16 if args.dtype == "fp16" else torch.bfloat16
-        prep = lambda b: preprocess_batch(b[0], b[1], b[2], device, dtype=act)  # noqa: E731
+        from can_distributed_pytorch_amd.ops.preprocess import preprocess_packed
+        prep = lambda b: preprocess_packed(b, device, dtype=act)  # noqa: E731
 
     model = CANNet(vgg16_path=args.vgg16 or None, backend="hip" if args.impl == "hip" else "torch",
                    batch_norm=args.batch_norm)
