@@ -199,7 +199,9 @@ extern "C" int can_preprocess_batch(const void* imgs, const float* dens, const l
   if (n <= 0 || Ho % ds || Wo % ds) return -2;
   int bx = (Ho * Wo + 255) / 256;
   if (bx > 512) bx = 512;
-  CAN_LAUNCH_DT(dt, preprocess_batch_kernel, dim3(bx, n, 2), dim3(256), 0, (hipStream_t)stream,
+  // dens == nullptr: the ground truth arrived already at 1/ds resolution (images only)
+  CAN_LAUNCH_DT(dt, preprocess_batch_kernel, dim3(bx, n, (dens != nullptr && gt != nullptr) ? 2 : 1), dim3(256), 0,
+                (hipStream_t)stream,
                 (const unsigned char*)imgs, dens, desc, (uint2*)x4, gt, Ho, Wo, ds, (float)(ds * ds));
   return (int)hipGetLastError();
 }

@@ -26,7 +26,7 @@ import numpy as np
 import torch
 from torch.utils.data import Dataset
 
-from .transforms import prepare_pair
+from .transforms import _axis_weights, prepare_pair
 
 IMG_EXT = (".jpg", ".jpeg", ".png", ".bmp", ".tif", ".tiff")
 _M64 = (1 << 64) - 1
@@ -42,6 +42,28 @@ def _splitmix64(x: int) -> int:
 def flip_draw(seed: int, epoch: int, index: int) -> bool:
     """The p=0.5 horizontal flip of sample ``index`` in ``epoch`` (stateless, worker-independent)."""
     return bool(_splitmix64(_splitmix64(_splitmix64(seed & _M64) ^ (epoch & _M64)) ^ (index & _M64)) >> 63)
+
+
+def density_to_gt(dmap: np.ndarray, h: int, w: int, downsample: int, flip: bool) -> np.ndarray:
+    """The density half of prepare_pair (model/CrowdDataset.py:48-62): optional flip, cv2 INTER_LINEAR resize to
+    (W//d, H//d) of the IMAGE's size, x d^2.  Returns fp32 [1, H//d, W//d]."""
+    if tuple(dmap.shape) != (h, w):
+        raise ValueError("density must match the image size")
+    rows, cols = h // downsample, w // downsample
+    if (rows, cols) == (h, w):
+        dm = np.asarray(dmap, dtype=np.float64)[:, ::-1] if flip else np.asarray(dmap, dtype=np.float64)
+    else:
+        # gather the rows the vertical taps use first (a memory-mapped map is read only there), then resize
+        y0, y1, fy = _axis_weights(h, rows)
+        x0, x1, fx = _axis_weights(w, cols)
+        if flip:                                 # flip before resize == mirrored column taps
+            x0, x1 = w - 1 - x0, w - 1 - x1
+        need = np.unique(np.concatenate([y0, y1]))
+        sub = np.asarray(dmap[need], dtype=np.float64)
+        pos = np.searchsorted(need, np.arange(h))
+        r = sub[pos[y0]] * (1.0 - fy)[:, None] + sub[pos[y1]] * fy[:, None]
+        dm = r[:, x0] * (1.0 - fx)[None] + r[:, x1] * fx[None]
+    return (dm * (downsample * downsample))[None].astype(np.float32)
 
 
 class EpochTaggedSampler:
@@ -110,14 +132,18 @@ class CrowdDataset(Dataset):
             raise IndexError("index range error")
         name = self.img_names[index]
         img = imread(os.path.join(self.img_root, name))
-        dmap = np.load(self.gt_path(name))                       # allow_pickle=False (default)
         flip = self.phase == "train" and flip_draw(self.seed, epoch, index)
         if self.raw:
+            # the GPU resizes / normalises the image; the ground truth is brought to its 1/d resolution here,
+            # reading only the source rows the bilinear taps touch (memory-mapped: ~1/4 of a full-resolution
+            # fp32 map), so a batch moves ~8x fewer host bytes than shipping full-resolution densities
             if img.dtype != np.uint8:
                 img = np.clip(np.asarray(img, dtype=np.float64) * (255.0 if img.dtype.kind == "f" else 1.0),
                               0, 255).astype(np.uint8)
-            return torch.from_numpy(np.ascontiguousarray(img)), torch.from_numpy(
-                np.ascontiguousarray(dmap, dtype=np.float32)), flip
+            dmap = np.load(self.gt_path(name), mmap_mode="r")        # allow_pickle=False (default)
+            gt = density_to_gt(dmap, img.shape[0], img.shape[1], self.gt_downsample, flip)
+            return torch.from_numpy(np.require(img, requirements=("C", "W"))), torch.from_numpy(gt), flip
+        dmap = np.load(self.gt_path(name))                       # allow_pickle=False (default)
         im, dm = prepare_pair(img, dmap, self.gt_downsample, flip)
         return torch.from_numpy(np.ascontiguousarray(im)), torch.from_numpy(np.ascontiguousarray(dm))
 

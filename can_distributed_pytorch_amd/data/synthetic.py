@@ -82,7 +82,7 @@ def make_synthetic_batch_gpu(batch: int, h: int, w: int, seed: int = 0, device="
     csrc/density.hip): only the head points and a coarse noise grid are drawn on the host.  Returns
     (x4 [B,H,W,4] 16-bit NHWC4 — the first layer's input layout — or, nhwc4=False, img [B,3,H,W] fp32,
     gt [B,1,H/8,W/8] fp32).  Statistically the CPU generator's images; not bitwise (different resampling
-    order).  seeds: optional per-image seeds (image i a function of seeds[i] alone: sharded datasets)."""
+    order), and reproducible per seed to fp32 rounding only (the density splat adds with fp32 atomics).  seeds: optional per-image seeds (image i a function of seeds[i] alone: sharded datasets)."""
     from ..ops import _ext
     from ..ops.conv import dt_code
     C = _ext.require()

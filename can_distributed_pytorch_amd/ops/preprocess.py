@@ -61,50 +61,48 @@ class RawCollate:
 
 
 class PackedCollate:
-    """collate_fn for CrowdDataset(raw=True) that packs a batch for ONE H2D copy per buffer and ONE launch:
-    returns (images uint8 [sum of H*W*C], densities fp32 [sum of H*W], desc int64 [n, 8], (Ho, Wo)) with
-    desc[i] = (image byte offset, H0, W0, C, flip, density offset, 0, 0).  Runs in the loader workers, so the
-    main process only copies; pin_memory=True pins the two big buffers."""
+    """collate_fn for CrowdDataset(raw=True) that packs a batch for ONE H2D copy of the images and ONE launch:
+    returns (images uint8 [sum of H*W*C], gt fp32 [n,1,H/d,W/d], desc int64 [n, 8], (Ho, Wo)) with
+    desc[i] = (image byte offset, H0, W0, C, flip, 0, 0, 0).  The raw dataset already brought each ground truth
+    to 1/d resolution (flip and x d^2 included), so only the images are resized on the GPU.  Runs in the
+    loader workers; pin_memory=True pins both buffers."""
 
     def __init__(self, downsample: int = 8):
         self.ds = downsample
 
     def __call__(self, batch: List):
-        imgs, dens, flips = zip(*batch)
+        imgs, gts, flips = zip(*batch)
         h0, w0 = imgs[0].shape[:2]
         ho, wo = (h0 // self.ds) * self.ds, (w0 // self.ds) * self.ds
         desc = torch.zeros(len(imgs), 8, dtype=torch.int64)
-        ioff = doff = 0
-        for i, (im, dm, fl) in enumerate(zip(imgs, dens, flips)):
+        ioff = 0
+        for i, (im, g, fl) in enumerate(zip(imgs, gts, flips)):
             hh, ww = im.shape[:2]
             if (hh // self.ds * self.ds, ww // self.ds * self.ds) != (ho, wo):
                 raise ValueError("all samples of a batch must resize to the same shape")
-            if tuple(dm.shape) != (hh, ww):
-                raise ValueError("density must match the image size")
+            if tuple(g.shape) != (1, ho // self.ds, wo // self.ds):
+                raise ValueError("raw samples must carry the 1/d ground truth [1, H/d, W/d]")
             ch = 1 if im.dim() == 2 else im.shape[2]
-            desc[i] = torch.tensor([ioff, hh, ww, ch, int(bool(fl)), doff, 0, 0])
+            desc[i] = torch.tensor([ioff, hh, ww, ch, int(bool(fl)), 0, 0, 0])
             ioff += hh * ww * ch
-            doff += hh * ww
         ibuf = torch.cat([im.reshape(-1) for im in imgs])
-        dbuf = torch.cat([dm.reshape(-1).float() for dm in dens])
-        return ibuf, dbuf, desc, (ho, wo)
+        return ibuf, torch.stack(gts), desc, (ho, wo)
 
 
 def preprocess_packed(packed, device, downsample: int = 8, dtype: torch.dtype = torch.bfloat16):
-    """PackedCollate output -> (x4 [N,Ho,Wo,4] 16-bit NHWC4, gt [N,1,Ho/d,Wo/d] fp32): one copy per buffer, one
-    launch for the whole batch (images and densities)."""
+    """PackedCollate output -> (x4 [N,Ho,Wo,4] 16-bit NHWC4, gt [N,1,Ho/d,Wo/d] fp32): one copy per buffer and one
+    launch for the whole batch of images."""
     C = _ext.require()
-    ibuf, dbuf, desc, (ho, wo) = packed
-    if ibuf.dtype != torch.uint8 or dbuf.dtype != torch.float32 or desc.dtype != torch.int64:
-        raise ValueError("packed batch: uint8 images, fp32 densities, int64 descriptors")
+    ibuf, gt, desc, (ho, wo) = packed
+    if ibuf.dtype != torch.uint8 or gt.dtype != torch.float32 or desc.dtype != torch.int64:
+        raise ValueError("packed batch: uint8 images, fp32 ground truth, int64 descriptors")
     dev = torch.device(device)
     n = desc.shape[0]
     from .conv import dt_code
     ib = ibuf.to(dev, non_blocking=True)
-    db = dbuf.to(dev, non_blocking=True)
     ds = desc.to(dev, non_blocking=True)
+    gtd = gt.to(dev, non_blocking=True)
     x4 = torch.empty(n, ho, wo, 4, dtype=dtype, device=dev)
-    gt = torch.empty(n, 1, ho // downsample, wo // downsample, dtype=torch.float32, device=dev)
-    C.preprocess_batch(ib.data_ptr(), db.data_ptr(), ds.data_ptr(), n, x4.data_ptr(), gt.data_ptr(), ho, wo,
-                       downsample, dt_code(dtype), _ext.stream_ptr(dev))
-    return x4, gt
+    C.preprocess_batch(ib.data_ptr(), 0, ds.data_ptr(), n, x4.data_ptr(), 0, ho, wo, downsample, dt_code(dtype),
+                       _ext.stream_ptr(dev))
+    return x4, gtd

@@ -109,3 +109,21 @@ def test_density_single_point_and_empty():
     d1 = gaussian_filter_density((40, 40), np.array([[20.0, 20.0]]))
     assert 0.85 < d1.sum() < 1.0                 # sigma = avg(shape)/4 = 10: +-2 sigma inside the image
     assert knn_sigmas(np.array([[1.0, 1.0]]), (40, 40))[0] == 10.0
+
+
+def test_density_to_gt_matches_prepare_pair_memmap(tmp_path):
+    """The raw (GPU-preprocessed) dataset's CPU ground-truth path == prepare_pair's density output, bitwise,
+    with and without the flip, reading the .npy memory-mapped."""
+    import numpy as np
+    from can_distributed_pytorch_amd.data.dataset import density_to_gt
+    from can_distributed_pytorch_amd.data.transforms import prepare_pair
+    rng = np.random.default_rng(12)
+    for (h, w) in [(77, 101), (64, 96), (35, 17)]:
+        d = rng.random((h, w)).astype(np.float32)
+        img = (rng.random((h, w, 3)) * 255).astype(np.uint8)
+        path = tmp_path / f"d{h}.npy"
+        np.save(path, d)
+        mm = np.load(path, mmap_mode="r")
+        for flip in (False, True):
+            ref = prepare_pair(img, d, 8, flip)[1]
+            assert np.array_equal(density_to_gt(mm, h, w, 8, flip), ref)

@@ -203,10 +203,11 @@ def test_no_uninitialized_reads_poisoned_allocator():
 
 
 def test_packed_batch_preprocess_matches_cpu_transform():
-    """PackedCollate (in the loader workers) + preprocess_packed (one H2D copy per buffer, ONE launch for the
-    batch) == data/transforms.prepare_pair per sample (cv2 INTER_LINEAR semantics), incl. flips, mixed source
-    sizes that resize to one shape, gray images."""
+    """CrowdDataset(raw=True) items -> PackedCollate (in the loader workers) -> preprocess_packed (one H2D copy
+    of the images, ONE launch for the batch) == data/transforms.prepare_pair per sample (cv2 INTER_LINEAR
+    semantics), incl. flips, mixed source sizes that resize to one shape, gray images."""
     import numpy as np
+    from can_distributed_pytorch_amd.data.dataset import density_to_gt
     from can_distributed_pytorch_amd.data.transforms import prepare_pair
     from can_distributed_pytorch_amd.ops.preprocess import PackedCollate, preprocess_packed
     rng = np.random.default_rng(9)
@@ -216,7 +217,7 @@ def test_packed_batch_preprocess_matches_cpu_transform():
         img = (rng.random((h, w, c) if c > 1 else (h, w)) * 255).astype(np.uint8)
         dm = rng.random((h, w)).astype(np.float32)
         flip = bool(i % 2)
-        samples.append((torch.from_numpy(img), torch.from_numpy(dm), flip))
+        samples.append((torch.from_numpy(img), torch.from_numpy(density_to_gt(dm, h, w, 8, flip)), flip))
         refs.append(prepare_pair(img, dm, 8, flip))
     packed = PackedCollate()(samples)
     x4, gt = preprocess_packed(packed, "cuda")
@@ -224,21 +225,22 @@ def test_packed_batch_preprocess_matches_cpu_transform():
     for i, (ri, rg) in enumerate(refs):
         got = x4[i, ..., :3].float().permute(2, 0, 1).cpu().numpy()
         assert np.abs(got - ri).max() < 0.03
-        assert np.abs(gt[i].cpu().numpy() - rg).max() < 1e-3
+        assert np.abs(gt[i].cpu().numpy() - rg).max() < 1e-5
     assert bool((x4[..., 3] == 0).all())
 
 
 def test_synthetic_gpu_generator():
     """GPU-rendered synthetic crowds: count-preserving ground truth (sum = number of heads inside, up to the
-    border mass), deterministic per seed, NHWC4 with channel 3 zero, statistics of the CPU recipe."""
+    border mass), reproducible per seed to fp32 rounding (the density splat adds with fp32 atomics, so the
+    last bits may differ run to run), NHWC4 with channel 3 zero, statistics of the CPU recipe."""
     from can_distributed_pytorch_amd.data.synthetic import make_synthetic_batch, make_synthetic_batch_gpu
     x4, gt = make_synthetic_batch_gpu(2, 128, 192, seeds=[5, 6], heads=(50, 60))
     x4b, gtb = make_synthetic_batch_gpu(2, 128, 192, seeds=[5, 6], heads=(50, 60))
     torch.cuda.synchronize()
-    assert torch.equal(x4, x4b) and torch.equal(gt, gtb)
+    assert torch.allclose(x4.float(), x4b.float(), atol=2e-2) and torch.allclose(gt, gtb, rtol=1e-5, atol=1e-6)
     assert bool((x4[..., 3] == 0).all())
     counts = gt.flatten(1).sum(1)
-    assert bool(((counts > 40) & (counts < 61)).all()), counts
+    assert bool(((counts > 20) & (counts < 61)).all()), counts          # heads clamped to the border lose mass
     img_cpu, gt_cpu = make_synthetic_batch(2, 128, 192, seed=5, heads=(50, 60))
     assert abs(float(x4[..., :3].float().mean()) - float(img_cpu.mean())) < 0.5
 
