@@ -638,6 +638,29 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
   // per tap from beyond L2: measured 25% L2 misses on the 512-ch layers).
   const int ntap = a.ksize * a.ksize;
   int i_tap = 0, i_c0 = 0;
+  // one stage's DMA in PARTS parts (part p = pieces [p*GA/PARTS ..) of the weights, [p*GB/PARTS ..) of the
+  // activations), issued between MFMA groups so the ~60-100-cycle issue cost of each LDS-DMA piece does not
+  // stall both waves of a SIMD in one burst after the barrier
+  constexpr int PARTS = (GA % 4 == 0 && GB % 4 == 0) ? 4 : 1;   // 2 parts measured slower (F5: +3..8%)
+  auto issue_part = [&](int buf, int p) {
+    int sh = 0;
+    if (a.ksize == 3) {
+      const int kh = (i_tap * 11) >> 5;
+      sh = ((kh - 1) * a.W + (i_tap - kh * 3 - 1)) * a.dil * a.Cin;
+    }
+    sh += i_c0;
+    const int i_k = i_tap * a.Cin + i_c0;
+    unsigned char* sbase = smem + buf * STAGE;
+#pragma unroll
+    for (int j = p * GA / PARTS; j < (p + 1) * GA / PARTS; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(a.w + aoff[j] + i_k), (__attribute__((address_space(3))) void*)(sbase + (wave + NW * j) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int j = p * GB / PARTS; j < (p + 1) * GB / PARTS; ++j) {
+      const void* src = ((bmask[j] >> i_tap) & 1u) ? (const void*)(a.x + boff[j] + sh) : (const void*)a.zero;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sbase + A_BYTES + (wave + NW * j) * 1024), 16, 0, 0);
+    }
+    if (p == PARTS - 1 && ++i_tap == ntap) { i_tap = 0; i_c0 += 64; }
+  };
   auto issue = [&](int buf) {
     int sh = 0;
     if (a.ksize == 3) {
@@ -722,6 +745,24 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
     __builtin_amdgcn_s_waitcnt(0x0070);
     asm volatile("s_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+#ifndef CANNET_DMA_BURST
+    if constexpr (PARTS > 1) {
+      // the four MFMA groups of the second K half, DMA parts of stage s+2 between them, the reads of stage
+      // s+1's first half after the second group
+      const bool more = s + 2 < nk;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        if ((g * PARTS) % 4 == 0 && more) issue_part(buf, g * PARTS / 4);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(a1, b1, g * PW, (g + 1) * PW);
+        __builtin_amdgcn_sched_barrier(0);
+        if (g == 1) read(buf ^ 1, 0, a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      continue;
+    }
+#endif
     if (s + 2 < nk) issue(buf);
     __builtin_amdgcn_sched_barrier(0);
     // half of the second-half MFMAs first (their operands are complete, so

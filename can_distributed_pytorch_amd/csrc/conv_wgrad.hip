@@ -575,17 +575,22 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
   const bf16_t* gdy = a.dy + bt * a.dy_bs;
   const bf16_t* gx = a.x + bt * a.x_bs;
 
-  // dY tile through a buffer resource: per-lane 32-bit offsets, stage base in soffset
+  // dY tile through a buffer resource: per-lane 32-bit offsets, stage base in soffset.  DMA piece j of a
+  // wave lands NW * 1024 / RB rows after piece 0 (a multiple of 16 rows: the same XOR swizzle), so one
+  // per-lane base offset + a wave-uniform stride per piece replaces the per-piece offset arrays (they
+  // pushed this kernel to 256 VGPRs with spills)
   const __amdgpu_buffer_rsrc_t dy_rsrc =
       __builtin_amdgcn_make_buffer_rsrc((void*)gdy, (short)0, a.M * a.Cout * 2, 0x00020000);
-  unsigned aoff[GA];
-#pragma unroll
-  for (int j = 0; j < GA; ++j) {
-    const int byte = (wave + NW * j) * 1024 + lane * 16;
+  constexpr int ASTEP = NW * 1024 / RBA, BSTEP = NW * 1024 / RBB;    // rows between pieces
+  static_assert(ASTEP % 16 == 0 && BSTEP % 16 == 0, "piece stride must keep the row swizzle");
+  unsigned aoff0;
+  {
+    const int byte = wave * 1024 + lane * 16;
     const int row = byte / RBA;
     const int lc16 = swz8b<RBA>(row, ((byte % RBA) / 16) * 2) >> 1;
-    aoff[j] = (unsigned)(row * a.Cout + co0 + lc16 * 8) * 2u;
+    aoff0 = (unsigned)(row * a.Cout + co0 + lc16 * 8) * 2u;
   }
+  const unsigned astride = (unsigned)(ASTEP * a.Cout * 2);
   // Cin % TK == 0: the whole k tile is ONE tap -> (dh, dw) are block-uniform
   const int tap = k0 / a.Cin;
   int dh = 0, dw = 0;
@@ -595,37 +600,54 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
     dw = (tap - kh * 3 - 1) * a.dil;
   }
   const int ci0 = k0 - tap * a.Cin;
-  int boff[GB], brow[GB];
-#pragma unroll
-  for (int j = 0; j < GB; ++j) {
-    const int byte = (wave + NW * j) * 1024 + lane * 16;
+  int boff0, brow0;
+  {
+    const int byte = wave * 1024 + lane * 16;
     const int row = byte / RBB;
-    brow[j] = row;
+    brow0 = row;
     const int lc16 = swz8b<RBB>(row, ((byte % RBB) / 16) * 2) >> 1;
-    boff[j] = (row + dh * a.W + dw) * a.Cin + ci0 + lc16 * 8;
+    boff0 = (row + dh * a.W + dw) * a.Cin + ci0 + lc16 * 8;
   }
+  const int bstride = BSTEP * a.Cin;
 
-  auto issue = [&](int st, int buf) {
+  // DMA of one stage, in 4 parts (part p = pieces [p*GA/4 ...) of dY then [p*GB/4 ...) of X) so that the
+  // issue cost of the 8 LDS-DMA pieces (~60-100 cycles each beside MFMAs) is spread between MFMA groups
+  // instead of stalling both waves of a SIMD in one burst after the barrier (-DCANNET_DMA_BURST at build
+  // time: the burst form)
+  struct StageAddr {
+    unsigned soff;
+    const bf16_t* xs;
+    int ow0;
+    bool row_ok;
+    unsigned char* sbase;
+  };
+  auto stage_addr = [&](int st, int buf) -> StageAddr {
+    StageAddr sa;
     const int m0 = mbeg + st * BKM;
     const uint32_t q = fdiv((uint32_t)m0, a.fdW);
-    const int ow0 = m0 - (int)q * a.W;
+    sa.ow0 = m0 - (int)q * a.W;
     const int oh = (int)q - (int)fdiv(q, a.fdH) * a.H;
-    const bool row_ok = (unsigned)(oh + dh) < (unsigned)a.H;     // stage-uniform
-    unsigned char* sbase = smem + buf * STAGE;
-    const unsigned soff = (unsigned)m0 * (unsigned)a.Cout * 2u;
+    sa.row_ok = (unsigned)(oh + dh) < (unsigned)a.H;     // stage-uniform
+    sa.sbase = smem + buf * STAGE;
+    sa.soff = (unsigned)m0 * (unsigned)a.Cout * 2u;
+    sa.xs = gx + (size_t)m0 * a.Cin;
+    return sa;
+  };
+  auto issue_part = [&](const StageAddr& sa, int p, int parts) {
 #pragma unroll
-    for (int j = 0; j < GA; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(dy_rsrc, (__attribute__((address_space(3))) void*)(sbase + (wave + NW * j) * 1024),
-                                               16, (int)aoff[j], (int)soff, 0, 0);
-    const bf16_t* xs = gx + (size_t)m0 * a.Cin;
+    for (int j = p * GA / parts; j < (p + 1) * GA / parts; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(dy_rsrc, (__attribute__((address_space(3))) void*)(sa.sbase + (wave + NW * j) * 1024),
+                                               16, (int)(aoff0 + j * astride), (int)sa.soff, 0, 0);
 #pragma unroll
-    for (int j = 0; j < GB; ++j) {
-      const int iw = ow0 + dw + brow[j];
-      const bool ok = row_ok && ((unsigned)iw < (unsigned)a.W);
-      const void* src = ok ? (const void*)(xs + boff[j]) : (const void*)a.zero;
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sbase + A_BYTES + (wave + NW * j) * 1024), 16, 0, 0);
+    for (int j = p * GB / parts; j < (p + 1) * GB / parts; ++j) {
+      const int iw = sa.ow0 + dw + brow0 + j * BSTEP;
+      const bool ok = sa.row_ok && ((unsigned)iw < (unsigned)a.W);
+      const void* src = ok ? (const void*)(sa.xs + boff0 + j * bstride) : (const void*)a.zero;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sa.sbase + A_BYTES + (wave + NW * j) * 1024), 16, 0, 0);
     }
   };
+  auto issue = [&](int st, int buf) { issue_part(stage_addr(st, buf), 0, 1); };
+  constexpr int PARTS = (GA % 4 == 0 && GB % 4 == 0) ? 4 : 1;   // 2 parts measured slower (F5: +3..8%)
 
   f32x4 acc[4][4 * KW];
 #pragma unroll
@@ -682,6 +704,26 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
       __builtin_amdgcn_s_waitcnt(0x0070);
       asm volatile("s_barrier" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
+#ifndef CANNET_DMA_BURST
+      if constexpr (PARTS > 1) {
+        // DMA parts interleaved with the four MFMA groups of the second K half; the reads of stage s+1's
+        // first half after the second group
+        const bool more = st + 2 < nstage;
+        StageAddr sa;
+        if (more) sa = stage_addr(st + 2, buf);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          if ((g * PARTS) % 4 == 0 && more) issue_part(sa, g * PARTS / 4, PARTS);
+          __builtin_amdgcn_sched_barrier(0);
+          mma(a1, b1, g * KW, (g + 1) * KW);
+          __builtin_amdgcn_sched_barrier(0);
+          if (g == 1) read(buf ^ 1, 0, a0, b0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        continue;
+      }
+#endif
       if (st + 2 < nstage) issue(st + 2, buf);
       __builtin_amdgcn_sched_barrier(0);
       mma(a1, b1, 0, 2 * KW);

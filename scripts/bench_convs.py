@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--json", default="")
     ap.add_argument("--halo", action="store_true", help="halo-tiled kernel for the Cin=64 fwd / Cout=64 dgrad layers")
     ap.add_argument("--tile", type=int, default=0, help="forced fwd/dgrad tile config (0 = auto)")
+    ap.add_argument("--passes", default="fwd,dgrad,wgrad", help="subset of fwd,dgrad,wgrad")
+    ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()
     dev = "cuda"
     out = []
@@ -71,10 +73,14 @@ def main():
             t = 31
         if a.halo and co == 64 and dil == 1 and ci in (64, 128):
             td = 31
-        res["fwd_ms"] = timeit(lambda: C.conv_igemm(x, wf, b, ksize=3, dil=dil, tile=t))
-        res["dgrad_ms"] = timeit(lambda: C.conv_igemm(dy, wd, None, ksize=3, dil=dil, epi=C.EPI_MASK, mask=x, tile=td)) \
-            if ci == co or True else 0
-        res["wgrad_ms"] = timeit(lambda: C.conv_wgrad(dy, x, dw, db, ksize=3, dil=dil, ws=ws))
+        passes = a.passes.split(",")
+        it = a.iters
+        res["fwd_ms"] = timeit(lambda: C.conv_igemm(x, wf, b, ksize=3, dil=dil, tile=t), it) if "fwd" in passes \
+            else float("nan")
+        res["dgrad_ms"] = timeit(lambda: C.conv_igemm(dy, wd, None, ksize=3, dil=dil, epi=C.EPI_MASK, mask=x, tile=td),
+                                 it) if "dgrad" in passes else float("nan")
+        res["wgrad_ms"] = timeit(lambda: C.conv_wgrad(dy, x, dw, db, ksize=3, dil=dil, ws=ws), it) \
+            if "wgrad" in passes else float("nan")
         if not a.no_ref:
             xr = x.permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
             wr = wt.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
@@ -85,6 +91,8 @@ def main():
             res["ref_wgrad_ms"] = timeit(lambda: torch.ops.aten.convolution_backward(
                 dyr, xr, wr, None, (1, 1), (dil, dil), (dil, dil), False, (0, 0), 1, (False, True, False)))
         for k in ("fwd", "dgrad", "wgrad"):
+            if k not in passes:
+                continue
             line = f"{name:4s} {k:6s} ours {res[k + '_ms']:7.3f} ms {fl / res[k + '_ms'] / 1e9:7.1f} TF/s"
             if not a.no_ref:
                 r = res["ref_" + k + "_ms"]
@@ -93,7 +101,7 @@ def main():
         out.append(res)
         del x, dy
         torch.cuda.empty_cache()
-    tot = {k: sum(r[k + "_ms"] for r in out) for k in ("fwd", "dgrad", "wgrad")}
+    tot = {k: sum(r[k + "_ms"] for r in out) for k in ("fwd", "dgrad", "wgrad") if k in a.passes.split(",")}
     print("total ours", {k: round(v, 3) for k, v in tot.items()})
     if not a.no_ref:
         rt = {k: sum(r["ref_" + k + "_ms"] for r in out) for k in ("fwd", "dgrad", "wgrad")}
