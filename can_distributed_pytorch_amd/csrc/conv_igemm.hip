@@ -1121,6 +1121,213 @@ conv_halo64_kernel(HaloConvArgs a) {
 }
 
 // ===========================================================================
+// Weight-stationary persistent 3x3 / dilation-1 conv, Cin = Cout = 64 (conv1_2
+// forward, its data gradient, the fused-pool forward).  conv_halo64_kernel
+// re-fetches the 72 KB of weights per 4 x 64 tile (24576 tiles at batch 8:
+// 1.8 GB through the L2) and each tap waits on its weight DMA: ~14 us per tile
+// for 1.9 us of MFMA work.  Here each wave keeps its 32 output channels x 576 K
+// of weights in registers for the whole kernel (144 VGPRs, loaded once), one
+// block per CU walks a contiguous run of tiles DOWN a 64-column strip (the next
+// tile's halo shares 2 of its 6 rows with this one: L2 hits), and the halo of
+// tile k+1 streams into the other of two LDS buffers while tile k computes.
+// Waves: 8 = 4 rows x 2 channel halves (64 px x 32 co each, 8 accumulators).
+//
+// One s_waitcnt vmcnt(0) per tile, at its end, covers the next halo, this
+// tile's mask loads and the previous tile's stores, all issued a whole tile
+// earlier (a counted wait would be unsafe: loads and stores retire out of
+// order with respect to each other).
+// ===========================================================================
+template <int DT, int EPI>
+__global__ void __launch_bounds__(512, 1) conv_ws64_kernel(HaloConvArgs a) {
+  constexpr int TR = 4, TCOL = 64, HC = TCOL + 2, HPIX = (TR + 2) * HC;   // 396 halo pixels
+  constexpr int NHI = (HPIX + 7) / 8;                                      // 50 one-KiB DMA pieces
+  constexpr int HALO_BYTES = NHI * 1024;
+  static_assert(EPI == EPI_BIAS_RELU || EPI == EPI_BIAS || EPI == EPI_NONE || EPI == EPI_MASK ||
+                EPI == EPI_POOLFWD, "ws64 epilogues");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int r = wave >> 1, h = wave & 1;           // output row of the tile, channel half
+  const int chb = h * 32 + fq * 8;                 // this lane's 8 consecutive output channels
+
+  // contiguous tile run of this block; tile index t -> (n, tx, ty) with ty fastest (down a column strip)
+  const int ntile = a.N * a.tiles_y * a.tiles_x;
+  const int per = (ntile + gridDim.x - 1) / gridDim.x;
+  const int t0 = blockIdx.x * per;
+  const int t1 = min(ntile, t0 + per);
+  if (t0 >= t1) return;                            // whole block: no barrier reached
+
+  auto tile_org = [&](int t, int& n, int& oh0, int& ow0) {
+    const int ty = t % a.tiles_y;
+    const int rest = t / a.tiles_y;
+    ow0 = (rest % a.tiles_x) * TCOL;
+    n = rest / a.tiles_x;
+    oh0 = ty * TR;
+  };
+  auto issue_halo = [&](int t, unsigned char* buf) {
+    int n, oh0, ow0;
+    tile_org(t, n, oh0, ow0);
+    for (int i = wave; i < NHI; i += 8) {
+      const int hp = i * 8 + (lane >> 3);
+      const int hr = hp / HC, hc = hp - hr * HC;
+      const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
+      const void* src = a.zero;
+      if (hp < HPIX && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+        src = a.x + ((size_t)(n * a.H + ih) * a.W + iw) * 64 + (((lane & 7) ^ (hc & 7)) * 8);
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(buf + i * 1024), 16, 0, 0);
+    }
+  };
+
+  issue_halo(t0, smem);
+  // weights: A fragment (k-step ks = 2 * tap + kk, row block j) of this wave's 32 channels; A row
+  // R = j * 16 + fr holds channel h * 32 + (R >> 2 & 3) * 8 + (R >> 4) * 4 + (R & 3), so that D row
+  // j * 16 + fq * 4 + q (acc[j][.][q]) is channel chb + j * 4 + q
+  frag8_t wf[18][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int R = j * 16 + fr;
+    const int co = h * 32 + ((R >> 2) & 3) * 8 + (R >> 4) * 4 + (R & 3);
+    const bf16_t* wr = a.w + (size_t)co * 576 + fq * 8;
+#pragma unroll
+    for (int ks = 0; ks < 18; ++ks)
+      wf[ks][j] = __builtin_bit_cast(frag8_t, *reinterpret_cast<const uint4*>(wr + (ks >> 1) * 64 + (ks & 1) * 32));
+  }
+  float bias[8];
+  if constexpr (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS || EPI == EPI_POOLFWD) {
+    const float4 b0 = *reinterpret_cast<const float4*>(a.bias + chb);
+    const float4 b1 = *reinterpret_cast<const float4*>(a.bias + chb + 4);
+    bias[0] = b0.x; bias[1] = b0.y; bias[2] = b0.z; bias[3] = b0.w;
+    bias[4] = b1.x; bias[5] = b1.y; bias[6] = b1.z; bias[7] = b1.w;
+  }
+  // per-lane halo offsets (swizzle keyed by the halo column: (fr + kw) & 7 for every fragment)
+  int hoff[3][2];
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+      hoff[kw][kk] = (r * HC + fr + kw) * 128 + (((kk * 4 + fq) ^ ((fr + kw) & 7)) * 16);
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+
+  for (int t = t0, it = 0; t < t1; ++t, ++it) {
+    unsigned char* cur = smem + (it & 1) * HALO_BYTES;
+    if (t + 1 < t1) issue_halo(t + 1, smem + ((it + 1) & 1) * HALO_BYTES);
+    int n, oh0, ow0;
+    tile_org(t, n, oh0, ow0);
+    const int oh = oh0 + r;
+    const bool row_ok = oh < a.H;
+    uint4 mk[4];
+    if constexpr (EPI == EPI_MASK) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ow = ow0 + i * 16 + fr;
+        mk[i] = make_uint4(0u, 0u, 0u, 0u);
+        if (row_ok && ow < a.W)
+          mk[i] = *reinterpret_cast<const uint4*>(a.mask + ((size_t)(n * a.H + oh) * a.W + ow) * 64 + chb);
+      }
+    }
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 18; ++ks) {
+      const int tap = ks >> 1, kk = ks & 1, kh = tap / 3, kw = tap % 3;
+      frag8_t bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        bfr[i] = __builtin_bit_cast(frag8_t, *reinterpret_cast<const uint4*>(cur + hoff[kw][kk] + kh * HC * 128 +
+                                                                              i * 2048));
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[j][i] = mfma16<DT>(wf[ks][j], bfr[i], acc[j][i]);
+    }
+    // the next halo, this tile's mask loads and the previous tile's stores have all retired; every wave's
+    // reads of `cur` are done after the barrier
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int col = i * 16 + fr, ow = ow0 + col;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[j * 4 + q] = acc[j][i][q];
+      if constexpr (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS || EPI == EPI_POOLFWD) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          v[c] += bias[c];
+          if (EPI != EPI_BIAS) v[c] = fmaxf(v[c], 0.f);
+        }
+      }
+      if constexpr (EPI == EPI_MASK) {
+        const unsigned mw[4] = {mk[i].x, mk[i].y, mk[i].z, mk[i].w};
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+          v[c] = pos_bits((unsigned short)(mw[c >> 1] >> ((c & 1) * 16))) ? v[c] : 0.f;
+      }
+      const uint4 o = pack8h<DT>(v);
+      if (row_ok && ow < a.W && (EPI != EPI_POOLFWD || a.y != nullptr))
+        *reinterpret_cast<uint4*>(a.y + ((size_t)(n * a.H + oh) * a.W + ow) * 64 + chb) = o;
+      if constexpr (EPI == EPI_POOLFWD) {
+        // staging tile [4 rows][64 cols] x 128 B in `cur`, 16-B chunk c of column col at slot c ^ (col & 7)
+        reinterpret_cast<uint4*>(cur + (r * 64 + col) * 128)[(h * 4 + fq) ^ (col & 7)] = o;
+      }
+    }
+    if constexpr (EPI == EPI_POOLFWD) {
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      // 2 pooled rows x 32 pooled columns x 8 chunks of 8 channels = 512 outputs, one per thread; max of the
+      // stored (rounded) values and the first-max codes, exactly as maxpool_fwd_kernel from the stored map
+      const int c = tid & 7, pc = (tid >> 3) & 31, pr = tid >> 8;
+      float m[8], tv[4][8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {     // q = window position in ATen order (row * 2 + column)
+        const int rr = 2 * pr + (q >> 1), cc = 2 * pc + (q & 1);
+        unpack8h<DT>(reinterpret_cast<const uint4*>(cur + (rr * 64 + cc) * 128)[c ^ (cc & 7)], tv[q]);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) m[k] = fmaxf(fmaxf(tv[0][k], tv[1][k]), fmaxf(tv[2][k], tv[3][k]));
+      const size_t pp = (size_t)(n * (a.H >> 1) + (oh0 >> 1) + pr) * (a.W >> 1) + (ow0 >> 1) + pc;
+      *reinterpret_cast<uint4*>(a.yp + pp * 64 + c * 8) = pack8h<DT>(m);
+      if (a.codes != nullptr) {
+        uint32_t cw = 0u;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t first = (tv[0][k] == m[k]) ? 1u : (tv[1][k] == m[k]) ? 2u : (tv[2][k] == m[k]) ? 4u : 8u;
+          cw |= ((m[k] > 0.f) ? first : 0u) << (4 * k);
+        }
+        a.codes[pp * 8 + c] = cw;
+      }
+      // staging reads done before the next-but-one halo DMA overwrites `cur`
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+  }
+}
+
+template <int DT, int EPI>
+static int launch_ws64(const HaloConvArgs& a, hipStream_t s) {
+  constexpr size_t lds = 2 * (size_t)(((6 * 66) + 7) / 8) * 1024;
+  auto kfn = conv_ws64_kernel<DT, EPI>;
+  static int ncu = 0;
+  if (!ncu) {
+    CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    int dev = 0;
+    CAN_HIP_CHECK(hipGetDevice(&dev));
+    CAN_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  const int ntile = a.N * a.tiles_y * a.tiles_x;
+  const int per = (ntile + ncu - 1) / ncu;
+  const int grid = (ntile + per - 1) / per;       // every block gets a non-empty run
+  hipLaunchKernelGGL(kfn, dim3(grid), dim3(512), lds, s, a);
+  return (int)hipGetLastError();
+}
+
+// ws64 (weight-stationary) instead of the halo kernel for Cin = Cout = 64 (CANNET_WS64=0: halo kernel)
+static bool use_ws64() { return getenv("CANNET_WS64") == nullptr || getenv("CANNET_WS64")[0] != '0'; }
+
+// ===========================================================================
 // First layer (conv1_1: 3 -> 64, 3x3, input NHWC4 bf16 = 8 B per pixel).
 // Output-write bound (805 MB of bf16 activations at batch 8 x 768 x 1024), so
 // the kernel does the minimum around the stores: the 6 x 130-pixel input halo
@@ -1344,6 +1551,14 @@ static int conv_igemm_impl(const void* x, const void* w, const float* bias, cons
       const long long rows = (long long)N * h.tiles_y * h.tiles_x * rows_per_tile;
       if (rows <= bpart_cap) { h.bpart = bpart; if (bpart_rows) *bpart_rows = (int)rows; }
     }
+    if (narrow && h.bpart == nullptr && use_ws64()) {
+      switch (epi) {
+        case EPI_BIAS_RELU: return launch_ws64<DT, EPI_BIAS_RELU>(h, s);
+        case EPI_MASK: return launch_ws64<DT, EPI_MASK>(h, s);
+        case EPI_NONE: return launch_ws64<DT, EPI_NONE>(h, s);
+        case EPI_BIAS: return launch_ws64<DT, EPI_BIAS>(h, s);
+      }
+    }
 #define CAN_HALO_CASE(E) \
     if (epi == E) return (Cout == 128) ? launch_halo64<DT, 128, E, 128>(h, s) \
                          : narrow ? launch_halo64<DT, 64, E, 64>(h, s) : launch_halo64<DT, 64, E, 128>(h, s);
@@ -1401,6 +1616,7 @@ static int conv_pool_fwd_impl(const void* x, const void* w, const float* bias, v
     h.yp = (bf16_t*)yp; h.codes = (uint32_t*)codes; h.zero = conv_zero_page();
     if (!h.zero) return -10;
     h.N = N; h.H = H; h.W = W; h.tiles_x = W / 64; h.tiles_y = H / 4;
+    if (use_ws64()) return launch_ws64<DT, EPI_POOLFWD>(h, s);
     return launch_halo64<DT, 64, EPI_POOLFWD, 64>(h, s);
   }
   ConvArgs2 b;

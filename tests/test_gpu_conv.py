@@ -368,3 +368,46 @@ def test_dgrad_bias_partials_feed_wgrad(n, h, w, ci, co, dil, epi, dtype):
     # partials sum the unrounded fp32 values: equal to the rounded-dY column sums to rounding
     assert torch.allclose(db2, ref, rtol=2e-2, atol=2e-2 * ref.abs().mean().item())
     assert torch.allclose(db1, ref, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("epi", ["fwd", "bias", "none", "dgrad", "pool"])
+@pytest.mark.parametrize("n,h,w", [(2, 64, 640), (1, 61, 600), (3, 8, 1024), (1, 4, 64)])
+def test_ws64_matches_halo_kernel(n, h, w, epi, monkeypatch):
+    """Cin = Cout = 64 convs: the weight-stationary persistent kernel (several tiles per block, ragged tiles)
+    == the per-tile halo kernel (CANNET_WS64=0) bitwise — the same MFMA k order per output — and both == the
+    fp32 reference."""
+    from can_distributed_pytorch_amd.ops import conv as C
+    torch.manual_seed(13)
+    dev = "cuda"
+    x = torch.randn(n, h, w, 64, device=dev).to(torch.bfloat16)
+    wt = (torch.randn(64, 64, 3, 3, device=dev) * 0.05).to(torch.bfloat16).float()
+    b = torch.randn(64, device=dev)
+    mask = torch.randn(n, h, w, 64, device=dev).to(torch.bfloat16)
+    if epi == "pool" and (h % 4 or w % 64):
+        pytest.skip("fused pool: whole 4 x 64 tiles only")
+
+    def run():
+        if epi == "fwd":
+            return (C.conv_igemm(x, C.pack_weight_fwd(wt), b, ksize=3),)
+        if epi == "bias":
+            return (C.conv_igemm(x, C.pack_weight_fwd(wt), b, ksize=3, epi=C.EPI_BIAS),)
+        if epi == "none":
+            return (C.conv_igemm(x, C.pack_weight_fwd(wt), None, ksize=3, epi=C.EPI_NONE),)
+        if epi == "dgrad":
+            return (C.conv_igemm(x, C.pack_weight_dgrad(wt), None, ksize=3, epi=C.EPI_MASK, mask=mask),)
+        y, yp, codes = C.conv_pool_fwd(x, C.pack_weight_fwd(wt), b, ksize=3, codes=True)
+        return y, yp, codes
+
+    monkeypatch.setenv("CANNET_WS64", "1")
+    new = run()
+    monkeypatch.setenv("CANNET_WS64", "0")
+    old = run()
+    torch.cuda.synchronize()
+    for a_, b_ in zip(new, old):
+        assert torch.equal(a_, b_)
+    if epi in ("fwd", "pool"):
+        _close(new[0], _ref(x, wt, b, 1))
+    elif epi == "dgrad":
+        xr = torch.zeros(n, 64, h, w, device=dev, requires_grad=True)
+        (gx,) = torch.autograd.grad(F.conv2d(xr, wt, None, padding=1), xr, x.float().permute(0, 3, 1, 2))
+        _close(new[0], gx.permute(0, 2, 3, 1) * (mask.float() > 0))
