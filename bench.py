@@ -135,7 +135,8 @@ def main(argv=None) -> int:
     # ---- untimed diagnostics
     extra = {}
     red = getattr(trainer, "reducer", None)
-    if a.impl == "hip":
+    native = a.impl == "hip" and a.dtype != "fp32"       # hip + fp32 = split-bf16 convs under the torch step
+    if native:
         extra["reducer"] = None if red is None else red.transport
         extra["rccl_world"] = (red.comm.world if (red is not None and red.comm is not None) else
                                (1 if red is None else None))
@@ -181,7 +182,7 @@ def main(argv=None) -> int:
             "config": {"model": "CANNet", "global_batch": a.batch * world, "per_gpu_batch": a.batch,
                        "image_hw": [a.height, a.width], "seq_len": None,
                        "parallelism": f"dp{world}", "impl": a.impl,
-                       "graph": bool(a.graph) and a.impl == "hip", "bucket_mb": a.bucket_mb,
+                       "graph": bool(a.graph) and native, "bucket_mb": a.bucket_mb,
                        "optimizer": "SGD(m=0.95) fp32 master", "loss": "MSE(sum)"},
             "train_tflops_per_s": round(tflops, 2),
             "final_loss": loss,

@@ -48,6 +48,7 @@ int can_head_train(const void* y, const float* w, const float* b, const float* g
 int can_sgd_momentum(float* p, float* buf, const float* g, size_t n, float lr, float momentum, float gscale,
                      int first, float* flags, const float* lr_dev, void* stream);
 int can_grad_nonfinite(const float* g, size_t n, float* flags, void* stream);
+int can_split_x3(const float* src, void* dst, long long M, int C, int stride, int mode, int pattern, void* stream);
 int can_scale_update(const float* flags, float* scaler, int interval, float growth, float backoff, float max_scale,
                      void* stream);
 int can_pack_conv(const float* w, void* fwd, void* dgr, int Co, int Ci, int taps, int first, int dt, void* stream);

@@ -139,6 +139,10 @@ PYBIND11_MODULE(CAN_MODULE_NAME, m) {
                            (const float*)lr_dev, P(st)),
           "sgd_momentum");
   });
+  m.def("split_x3", [](uintptr_t src, uintptr_t dst, long long M, int C, int stride, int mode, int pattern,
+                       uintptr_t st) {
+    check(can_split_x3((const float*)src, (void*)dst, M, C, stride, mode, pattern, P(st)), "split_x3");
+  });
   m.def("grad_nonfinite", [](uintptr_t g, size_t n, uintptr_t flags, uintptr_t st) {
     check(can_grad_nonfinite((const float*)g, n, (float*)flags, P(st)), "grad_nonfinite");
   });

@@ -57,8 +57,11 @@ struct ConvArgs {
 // tile is then 2 image rows x TP/2 columns with the rows interleaved inside each 16-pixel MFMA fragment
 // (fragment f, row fr: column f*8 + fr/2, row fr&1), so every pool window sits in 4 adjacent lanes and is
 // reduced with two DPP quad permutes (the pooled map is never re-read from HBM by a separate pass).
+// EPI_F32 (LDS-DMA kernels only): the raw GEMM result (+ bias when a.bias is given) stored as fp32 into
+// a.y reinterpreted as float [M][Cout] — the split-bf16 fp32 path (ops/fp32.py) sums hi*hi + hi*lo + lo*hi
+// in one K-concatenated GEMM and needs the fp32 accumulator, not its 16-bit rounding.
 enum { EPI_BIAS_RELU = 0, EPI_MASK = 1, EPI_NONE = 2, EPI_BIAS = 3, EPI_SIGMOID = 4, EPI_POOLBWD = 5,
-       EPI_POOLFWD = 6 };
+       EPI_POOLFWD = 6, EPI_F32 = 7 };
 enum { LOAD_GENERIC = 0, LOAD_FIRST = 1 };
 
 
@@ -341,7 +344,7 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
   constexpr int TC = 64 * WC, TP = 64 * PW * WP;
   const int chb = ct * TC + wc * 64 + fq * 16;
   float bias[16];
-  if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS || EPI == EPI_POOLFWD) {
+  if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS || EPI == EPI_POOLFWD || (EPI == EPI_F32 && a.bias != nullptr)) {
 #pragma unroll
     for (int c = 0; c < 16; c += 4) {
       const float4 b4 = *reinterpret_cast<const float4*>(a.bias + chb + c);
@@ -399,6 +402,16 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
       for (int c = 0; c < 16; ++c) v[c] = 1.f / (1.f + __expf(-v[c]));
     }
     const size_t off = (size_t)m * a.Cout + chb;
+    if constexpr (EPI == EPI_F32) {
+      if (a.bias != nullptr) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) v[c] += bias[c];
+      }
+      float* yf = reinterpret_cast<float*>(a.y) + off;
+#pragma unroll
+      for (int c = 0; c < 16; c += 4) *reinterpret_cast<float4*>(yf + c) = make_float4(v[c], v[c + 1], v[c + 2], v[c + 3]);
+      continue;
+    }
     if (EPI == EPI_MASK) {
       const uint4 m0 = *reinterpret_cast<const uint4*>(a.mask + off);
       const uint4 m1 = *reinterpret_cast<const uint4*>(a.mask + off + 8);
@@ -1535,7 +1548,7 @@ static int conv_igemm_impl(const void* x, const void* w, const float* bias, cons
     return -5;
   }
   if (auto_halo && Cin == 64 && ksize == 3 && dil == 1 && (Cout == 64 || Cout == 128) && epi != EPI_SIGMOID &&
-      epi != EPI_POOLBWD)
+      epi != EPI_POOLBWD && epi != EPI_F32)
     tile_cfg = 31;
   if (tile_cfg == 31) {
     // halo-tiled Cin = 64 kernel (explicit; see conv_halo64_kernel)
@@ -1588,6 +1601,7 @@ static int conv_igemm_impl(const void* x, const void* w, const float* bias, cons
       case EPI_BIAS: return dispatch_glds<DT, EPI_BIAS>(b, tile_cfg, s);
       case EPI_SIGMOID: return dispatch_glds<DT, EPI_SIGMOID>(b, tile_cfg, s);
       case EPI_POOLBWD: return dispatch_glds<DT, EPI_POOLBWD>(b, tile_cfg, s);
+      case EPI_F32: return dispatch_glds<DT, EPI_F32>(b, tile_cfg, s);
     }
     return -6;
   }

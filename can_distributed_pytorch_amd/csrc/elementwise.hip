@@ -283,6 +283,35 @@ __global__ void __launch_bounds__(256) grad_nonfinite_kernel(const float4* __res
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<int*>(flag), 0x3f800000);   // 1.0f
 }
 
+// ---------------------------------------------------------------- split-bf16 (fp32 path)
+// x = hi + lo with hi = bf16(x), lo = bf16(x - hi): the fp32 path (ops/fp32.py) computes every conv GEMM as
+// hi*hi + hi*lo + lo*hi on the bf16 MFMA kernels with fp32 accumulation.  src fp32 [M][C]; three blocks,
+// block b = lo if bit b of `pattern` is set, else hi:
+//   mode 0 (K-concatenated operand): dst [M][stride], block b at channels [b*C, (b+1)*C), zero from 3*C on;
+//   mode 1 (M-stacked operand):      dst [3][M][stride], block b = rows [b*M, (b+1)*M), zero from C on.
+__global__ void __launch_bounds__(256) split_x3_kernel(const float* __restrict__ src, unsigned short* __restrict__ dst,
+                                                       long long M, int C, int stride, int mode, int pattern) {
+  const long long total = (mode == 0 ? 1 : 3) * M * (long long)stride;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const long long row = i / stride;
+    const int col = (int)(i - row * stride);
+    int b, c;
+    long long m;
+    if (mode == 0) {
+      m = row; b = col / C; c = col - b * C;
+    } else {
+      b = (int)(row / M); m = row - (long long)b * M; c = col;
+    }
+    unsigned short v = 0;
+    if (b < 3 && c < C) {
+      const float x = src[m * C + c];
+      const unsigned short hi = f2bf(x);
+      v = ((pattern >> b) & 1) ? f2bf(x - bf2f(hi)) : hi;
+    }
+    dst[i] = v;
+  }
+}
+
 __global__ void scale_update_kernel(const float* __restrict__ flag, float* __restrict__ scaler, int interval,
                                     float growth, float backoff, float max_scale) {
   if (threadIdx.x != 0) return;
@@ -454,6 +483,15 @@ extern "C" int can_grad_nonfinite(const float* g, size_t n, float* flag, void* s
   if (n & 3) return -2;
   hipLaunchKernelGGL(grad_nonfinite_kernel, dim3(grid_for(n / 4, 256, 2048)), dim3(256), 0, (hipStream_t)stream,
                      (const float4*)g, n / 4, flag);
+  return (int)hipGetLastError();
+}
+
+extern "C" int can_split_x3(const float* src, void* dst, long long M, int C, int stride, int mode, int pattern,
+                            void* stream) {
+  if (M < 1 || C < 1 || (mode == 0 && stride < 3 * C) || (mode == 1 && stride < C) || mode < 0 || mode > 1) return -2;
+  const size_t total = (size_t)(mode == 0 ? 1 : 3) * (size_t)M * (size_t)stride;
+  hipLaunchKernelGGL(split_x3_kernel, dim3(grid_for(total, 256, 8192)), dim3(256), 0, (hipStream_t)stream, src,
+                     (unsigned short*)dst, M, C, stride, mode, pattern);
   return (int)hipGetLastError();
 }
 

@@ -24,11 +24,13 @@ from ..models.cannet import CANNet
 
 
 class TorchStepper:
+    exec_backend = "torch"
+
     def __init__(self, device, dtype="fp32", world=1, lr=1e-7, momentum=0.95, channels_last=None, model=None,
                  bucket_mb: float = 25.0):
         self.device = torch.device(device)
-        self.model = (model or CANNet(backend="torch")).to(self.device)
-        self.model.exec_backend = "torch"
+        self.model = (model or CANNet(backend=self.exec_backend)).to(self.device)
+        self.model.exec_backend = self.exec_backend
         self.dtype = dtype
         self.channels_last = (dtype != "fp32") if channels_last is None else channels_last
         if self.channels_last:
@@ -70,11 +72,26 @@ class TorchStepper:
         return None if self._loss is None else float(self._loss)
 
 
+class Fp32Stepper(TorchStepper):
+    """fp32 training numerics (the reference's, train.py:126) on the native kernels: every convolution —
+    forward, data and weight gradient — runs as split-bf16 GEMMs on the MFMA conv kernels with fp32
+    accumulation (ops/fp32.py); ReLU / pooling / the context module's elementwise math, the loss, DDP and SGD
+    are the fp32 ATen / torch.distributed ones of TorchStepper."""
+    exec_backend = "hip_fp32"
+
+    def __init__(self, device, dtype="fp32", **kw):
+        if dtype != "fp32":
+            raise ValueError("Fp32Stepper is the fp32 step")
+        super().__init__(device, dtype="fp32", channels_last=False, **kw)
+
+
 def build_trainer(impl="hip", dtype="bf16", device="cuda", world=1, lr=1e-7, batch=8,
                   height=768, width=1024, graph=True, model=None, bucket_mb: float = 25.0,
                   reducer_transport: Optional[str] = None):
     if impl == "torch":
         return TorchStepper(device, dtype=dtype, world=world, lr=lr, model=model, bucket_mb=bucket_mb)
+    if dtype == "fp32":
+        return Fp32Stepper(device, world=world, lr=lr, model=model, bucket_mb=bucket_mb)
     from .native import NativeStepper
     return NativeStepper(device, dtype=dtype, world=world, lr=lr, batch=batch, height=height,
                          width=width, graph=graph, model=model, bucket_mb=bucket_mb,

@@ -77,13 +77,15 @@ class CANNet(nn.Module):
             Also read from ``$CANNET_VGG16`` when not given.
         backend: ``"auto"`` (native HIP executor on GPU tensors, ATen on CPU),
             ``"hip"`` (force native; raises on CPU), ``"torch"`` (plain ATen
-            graph everywhere — the stock-PyTorch reference stack).
+            graph everywhere — the stock-PyTorch reference stack), ``"hip_fp32"``
+            (fp32 training numerics: every convolution as split-bf16 on the
+            MFMA kernels, ops/fp32.py; GPU only).
     """
 
     def __init__(self, load_weights: bool = False, vgg16_path: Optional[str] = None,
                  backend: str = "auto", batch_norm: bool = False):
         super().__init__()
-        if backend not in ("auto", "hip", "torch"):
+        if backend not in ("auto", "hip", "torch", "hip_fp32"):
             raise ValueError(f"unknown backend {backend!r}")
         self.frontend_feat = list(FRONTEND_CFG)
         self.backend_feat = list(BACKEND_CFG)
@@ -161,6 +163,11 @@ class CANNet(nn.Module):
 
     # --------------------------------------------------------------- forward
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.exec_backend == "hip_fp32":
+            if not x.is_cuda:
+                raise RuntimeError("backend='hip_fp32' needs a GPU tensor")
+            from ..ops.fp32 import cannet_forward_fp32
+            return cannet_forward_fp32(self, x)
         if self._use_native(x):
             if self._executor is None:
                 from ..ops.executor import CANNetExecutor  # raises loudly if the HIP extension is missing

@@ -111,7 +111,7 @@ def make_loaders(args, world, rank, raw=False, device=None, dtype=None):
     # indices carry the epoch into (persistent) workers: the flip is a function of (seed, epoch, index)
     bs = BatchSampler(EpochTaggedSampler(train_sampler), args.batch_size, drop_last=False)
     if args.synthetic and device is not None and device.type == "cuda" and args.impl == "hip" and \
-            h % 16 == 0 and w % 16 == 0:
+            args.dtype != "fp32" and h % 16 == 0 and w % 16 == 0:
         from can_distributed_pytorch_amd.data.synthetic import SyntheticGPULoader
         train_loader = SyntheticGPULoader(bs, h, w, args.seed, device, dtype=dtype)
         test_loader = SyntheticGPULoader(BatchSampler(test_sampler, args.batch_size, drop_last=False), h, w,
@@ -134,9 +134,6 @@ def main(args):
     if args.impl == "hip" and not use_gpu:
         print("[no GPU: falling back to --impl torch on CPU]")
         args.impl = "torch"
-    if args.impl == "hip" and args.dtype == "fp32":
-        print("[--dtype fp32: the native kernels compute in bf16/fp16; using --impl torch]")
-        args.impl = "torch"
     if args.batch_norm and args.impl == "hip":
         print("[--batch-norm: the fused native step has no BN layers; using --impl torch]")
         args.impl = "torch"
@@ -148,7 +145,8 @@ def main(args):
     if rank == 0:
         print(f"[train start {time.strftime('%Y.%m.%d %H:%M:%S')}] world {world} impl {args.impl} {args}")
 
-    raw = bool(args.gpu_preprocess and args.impl == "hip" and not args.synthetic)
+    # the NHWC4 16-bit input layout the GPU preprocessing writes is the native bf16/fp16 step's
+    raw = bool(args.gpu_preprocess and args.impl == "hip" and args.dtype != "fp32" and not args.synthetic)
     act = torch.float16 if args.dtype == "fp16" else torch.bfloat16
     train_loader, test_loader, train_sampler, test_sampler = make_loaders(args, world, rank, raw=raw, device=device,
                                                                           dtype=act)
@@ -169,13 +167,15 @@ def main(args):
     from can_distributed_pytorch_amd.engine.trainer import build_trainer
     fixed = bool(args.synthetic)
     graph = bool(args.graph) and fixed
-    if args.impl == "hip":
+    if args.impl == "hip" and args.dtype != "fp32":
         stepper = build_trainer(impl="hip", dtype=args.dtype, device=device, world=world, lr=base_lr, graph=graph,
                                 model=model)
         net = stepper.model
         momentum = stepper.mom
     else:
-        stepper = build_trainer(impl="torch", dtype=args.dtype if use_gpu else "fp32", device=device, world=world,
+        # --impl torch: stock ATen / MIOpen; --impl hip --dtype fp32: split-bf16 convolutions on the native
+        # MFMA kernels (engine/trainer.Fp32Stepper), the rest of the step as the torch one
+        stepper = build_trainer(impl=args.impl, dtype=args.dtype if use_gpu else "fp32", device=device, world=world,
                                 lr=base_lr, model=model)
         if world > 1:
             for p in stepper.model.parameters():
