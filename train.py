@@ -169,14 +169,14 @@ def main(args):
     graph = bool(args.graph) and fixed
     if args.impl == "hip" and args.dtype != "fp32":
         stepper = build_trainer(impl="hip", dtype=args.dtype, device=device, world=world, lr=base_lr, graph=graph,
-                                model=model)
+                                model=model, bucket_mb=args.bucket_mb)
         net = stepper.model
         momentum = stepper.mom
     else:
         # --impl torch: stock ATen / MIOpen; --impl hip --dtype fp32: split-bf16 convolutions on the native
         # MFMA kernels (engine/trainer.Fp32Stepper), the rest of the step as the torch one
         stepper = build_trainer(impl=args.impl, dtype=args.dtype if use_gpu else "fp32", device=device, world=world,
-                                lr=base_lr, model=model)
+                                lr=base_lr, model=model, bucket_mb=args.bucket_mb)
         if world > 1:
             for p in stepper.model.parameters():
                 dist.broadcast(p.data, src=0)
