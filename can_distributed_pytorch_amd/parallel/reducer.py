@@ -99,18 +99,43 @@ class BucketedReducer:
             for i in bk.params:
                 self.param_bucket[i] = b
         self._native = None
+        self.comm = None
         if transport == "rccl":
             from ..ops import _ext
             C = _ext.require()
-            self.comm = comm or make_rccl_comm(dev, group)
-            self._native = C.BucketReducer(self.comm, arena.grad.data_ptr(),
-                                           [b.start for b in self.buckets], [b.numel for b in self.buckets],
-                                           self.param_bucket, 1)
-        else:
-            self.comm = None
+            self.comm = comm or self._make_comm_agreed(dev, group)
+            if self.comm is None:
+                self.transport = transport = "torch"      # every rank falls back together (see below)
+            else:
+                self._native = C.BucketReducer(self.comm, arena.grad.data_ptr(),
+                                               [b.start for b in self.buckets], [b.numel for b in self.buckets],
+                                               self.param_bucket, 1)
         self._pending = None
         self._next = 0
         self._works = []
+
+    def _make_comm_agreed(self, dev, group):
+        """This rank's RCCL communicator, or None on EVERY rank if any rank failed to create one: the ranks
+        agree through one all-reduce on the torch process group, and the reducer then runs its buckets through
+        torch.distributed (the same RCCL underneath, without the owned communicator) instead of training
+        with mismatched transports."""
+        comm, err = None, None
+        try:
+            comm = make_rccl_comm(dev, group)
+        except RuntimeError as e:                 # e.g. communicator init refused by RCCL
+            err = e
+        if self.world > 1:
+            ok = torch.tensor([0.0 if err is None else 1.0], device=dev)
+            dist.all_reduce(ok, group=group)
+            failed = ok.item() > 0
+        else:
+            failed = err is not None
+        if failed:
+            import warnings
+            warnings.warn(f"owned RCCL communicator unavailable ({err or 'failed on another rank'}); "
+                          "gradient buckets go through torch.distributed")
+            return None
+        return comm
 
     # --------------------------------------------------------------- step API
     def begin(self):
@@ -138,6 +163,8 @@ class BucketedReducer:
             self._next += 1
 
     def _launch(self, b: int):
+        if self.world < 2:                        # a 1-rank all-reduce is the identity
+            return
         bk = self.buckets[b]
         view = self.arena.grad[bk.start:bk.end]
         self._works.append(dist.all_reduce(view, group=self.group, async_op=True))

@@ -157,3 +157,24 @@ def test_fake_cluster_detects_divergent_plans(C):
         futs = [pool.submit(run, r) for r in range(2)]
         errs = [f.exception() for f in futs]
     assert any(e is not None and ("mismatch" in str(e) or "timed out" in str(e)) for e in errs), errs
+
+
+def test_rccl_comm_failure_falls_back_to_torch_transport(monkeypatch):
+    """If the owned RCCL communicator cannot be created, the reducer runs its buckets through torch.distributed
+    (world 1 here: no all-reduce needed) instead of failing the run or mixing transports across ranks."""
+    import warnings
+    from can_distributed_pytorch_amd.parallel import reducer as R
+    params = [torch.nn.Parameter(torch.randn(300)), torch.nn.Parameter(torch.randn(50))]
+    arena = FlatArena(params, torch.device("cpu"), order=[1, 0])
+
+    def boom(*a, **k):
+        raise RuntimeError("rccl init refused")
+    monkeypatch.setattr(R, "make_rccl_comm", boom)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        red = R.BucketedReducer(arena, [1, 0], bucket_mb=1.0, transport="rccl")
+    assert red.transport == "torch" and red.comm is None and red._native is None
+    assert any("torch.distributed" in str(x.message) for x in w)
+    red.begin()
+    red.mark_ready([1, 0])
+    red.finish()
