@@ -7,6 +7,9 @@
 extern "C" {
 #endif
 
+int can_conv_igemm_batched(const void* x, const void* w, const float* bias, void* y, int nb, long long xbs,
+                           long long wbs, long long ybs, int N, int H, int W, int Cin, int Cout, int ksize, int dil,
+                           int epi, int tile_cfg, int dt, void* stream);
 int can_conv_igemm(const void* x, const void* w, const float* bias, const void* mask, void* y, int N, int H, int W,
                    int Cin, int Cout, int ksize, int dil, int epi, int first, int tile_cfg, int dt, void* stream,
                    float* bpart, int bpart_cap, int* bpart_rows);

@@ -53,6 +53,13 @@ PYBIND11_MODULE(CAN_MODULE_NAME, m) {
      py::arg("W"), py::arg("Cin"), py::arg("Cout"), py::arg("ksize"), py::arg("dil"), py::arg("epi"), py::arg("first"),
      py::arg("tile_cfg"), py::arg("dt"), py::arg("stream"), py::arg("bpart") = 0, py::arg("bpart_cap") = 0);
 
+  m.def("conv_igemm_batched", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int nb, long long xbs,
+                                 long long wbs, long long ybs, int N, int H, int W, int Cin, int Cout, int ksize,
+                                 int dil, int epi, int tile_cfg, int dt, uintptr_t stream) {
+    check(can_conv_igemm_batched(P(x), P(w), (const float*)bias, P(y), nb, xbs, wbs, ybs, N, H, W, Cin, Cout, ksize,
+                                 dil, epi, tile_cfg, dt, P(stream)),
+          "conv_igemm_batched");
+  });
   m.def("wgrad_plan", [](int M, int Cin, int Cout, int ksize, int first, int target_blocks, int dil) {
     int S = 0, ms = 0, cfg = 0;
     check(can_wgrad_plan(M, Cin, Cout, ksize, first, target_blocks, &S, &ms, &cfg, dil), "wgrad_plan");

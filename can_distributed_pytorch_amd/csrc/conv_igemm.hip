@@ -321,6 +321,8 @@ struct ConvArgs2 {
   // EPI_MASK / EPI_POOLBWD (data gradient = the next layer's dY): bias-gradient partials of that dY,
   // [npt * WP][Cout] fp32, row = pixel tile * WP + wave's pixel slot (optional)
   float* bpart = nullptr;
+  // batched launch (v2 kernel): item blockIdx.y reads x + y*xbs, w + y*wbs and writes y + y*ybs (elements)
+  long long xbs = 0, wbs = 0, ybs = 0;
 };
 
 // pixel m of row r of pixel tile pt; EPI_POOLFWD tiles are 2 rows x TP/2 columns, rows interleaved per
@@ -592,6 +594,11 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds_kernel(ConvArgs2 a)
 // ===========================================================================
 template <int DT, int WC, int WP, int PW, int EPI>
 __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a) {
+  if (blockIdx.y) {                               // batched launch: item blockIdx.y
+    a.x += blockIdx.y * a.xbs;
+    a.w += blockIdx.y * a.wbs;
+    a.y += blockIdx.y * a.ybs;
+  }
   constexpr int NW = WC * WP;
   constexpr int TC = 64 * WC, TP = 64 * PW * WP;
   constexpr int A_BYTES = TC * 128, B_BYTES = TP * 128;
@@ -798,7 +805,7 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
 }
 
 template <int DT, int WC, int WP, int PW, int EPI>
-static int launch_glds2(const ConvArgs2& a, hipStream_t s) {
+static int launch_glds2(const ConvArgs2& a, hipStream_t s, int nb = 1) {
   constexpr int TC = 64 * WC, TP = 64 * PW * WP;
   const size_t lds = 2 * (size_t)(TC + TP) * 128;
   auto kfn = conv_glds2_kernel<DT, WC, WP, PW, EPI>;
@@ -808,7 +815,7 @@ static int launch_glds2(const ConvArgs2& a, hipStream_t s) {
     attr = true;
   }
   const int nct = a.Cout / TC, npt = (a.M + TP - 1) / TP;
-  hipLaunchKernelGGL(kfn, dim3(nct * npt), dim3(64 * WC * WP), lds, s, a);
+  hipLaunchKernelGGL(kfn, dim3(nct * npt, nb), dim3(64 * WC * WP), lds, s, a);
   return (int)hipGetLastError();
 }
 
@@ -1487,7 +1494,7 @@ static int glds_bpart_rows(int cfg, int M) {
 }
 
 template <int DT, int EPI>
-static int dispatch_glds(const ConvArgs2& a, int tile_cfg, hipStream_t s) {
+static int dispatch_glds(const ConvArgs2& a, int tile_cfg, hipStream_t s, int nb = 1) {
   int cfg = tile_cfg;
   if (cfg == 0) cfg = glds_default_cfg(a.Cin, a.Cout, a.ksize);
   if constexpr (EPI == EPI_POOLFWD) {
@@ -1498,13 +1505,13 @@ static int dispatch_glds(const ConvArgs2& a, int tile_cfg, hipStream_t s) {
     if (a.pcodes == nullptr) return -14;
   }
   switch (cfg) {
-    case 11: if (a.Cout % 256 || EPI == EPI_POOLFWD) return -8; return launch_glds<DT, 4, 2, 2, EPI>(a, s);
-    case 12: if (a.Cout % 128 || EPI == EPI_POOLFWD) return -8; return launch_glds<DT, 2, 4, 1, EPI>(a, s);
-    case 13: if (EPI == EPI_POOLFWD) return -8; return launch_glds<DT, 1, 8, 1, EPI>(a, s);
-    case 21: if (a.Cout % 256) return -8; return launch_glds2<DT, 4, 2, 2, EPI>(a, s);
-    case 22: if (a.Cout % 128) return -8; return launch_glds2<DT, 2, 4, 1, EPI>(a, s);
-    case 23: return launch_glds2<DT, 1, 8, 1, EPI>(a, s);
-    case 25: if (a.Cout % 128) return -8; return launch_glds2<DT, 2, 4, 2, EPI>(a, s);   // 128 x 512, 160 KB LDS
+    case 11: if (a.Cout % 256 || EPI == EPI_POOLFWD || nb > 1) return -8; return launch_glds<DT, 4, 2, 2, EPI>(a, s);
+    case 12: if (a.Cout % 128 || EPI == EPI_POOLFWD || nb > 1) return -8; return launch_glds<DT, 2, 4, 1, EPI>(a, s);
+    case 13: if (EPI == EPI_POOLFWD || nb > 1) return -8; return launch_glds<DT, 1, 8, 1, EPI>(a, s);
+    case 21: if (a.Cout % 256) return -8; return launch_glds2<DT, 4, 2, 2, EPI>(a, s, nb);
+    case 22: if (a.Cout % 128) return -8; return launch_glds2<DT, 2, 4, 1, EPI>(a, s, nb);
+    case 23: return launch_glds2<DT, 1, 8, 1, EPI>(a, s, nb);
+    case 25: if (a.Cout % 128) return -8; return launch_glds2<DT, 2, 4, 2, EPI>(a, s, nb);   // 128 x 512, 160 KB LDS
   }
   return -9;
 }
@@ -1614,6 +1621,31 @@ static int conv_igemm_impl(const void* x, const void* w, const float* bias, cons
   return -6;
 }
 
+// nb independent convs of one shape in ONE launch of the v2 kernel (grid.y = item): the context module's four
+// 512 -> 512 1x1 convs (sigmoid forward, plain data gradient).  Items are nb x the single-conv layout at
+// element strides xbs / wbs / ybs.
+template <int DT>
+static int conv_igemm_batched_impl(const void* x, const void* w, const float* bias, void* y, int nb, long long xbs,
+                                   long long wbs, long long ybs, int N, int H, int W, int Cin, int Cout, int ksize,
+                                   int dil, int epi, int tile_cfg, hipStream_t s) {
+  if (nb < 1 || nb > 65535 || Cin % 64 || Cout % 64 || H < 2 || W < 2) return -2;
+  if (tile_cfg != 0 && tile_cfg < 20) return -8;
+  ConvArgs2 b;
+  b.x = (const bf16_t*)x; b.w = (const bf16_t*)w; b.bias = bias; b.mask = nullptr; b.y = (bf16_t*)y;
+  b.zero = conv_zero_page();
+  if (!b.zero) return -10;
+  b.H = H; b.W = W; b.Cin = Cin; b.Cout = Cout; b.ksize = ksize; b.dil = dil; b.M = N * H * W;
+  b.fdW = make_fastdiv((uint32_t)W); b.fdH = make_fastdiv((uint32_t)H);
+  b.xbs = xbs; b.wbs = wbs; b.ybs = ybs;
+  const int cfg = tile_cfg ? tile_cfg : glds_default_cfg(Cin, Cout, ksize);   // always a v2 config
+  switch (epi) {
+    case EPI_NONE: return dispatch_glds<DT, EPI_NONE>(b, cfg, s, nb);
+    case EPI_SIGMOID: return dispatch_glds<DT, EPI_SIGMOID>(b, cfg, s, nb);
+    case EPI_BIAS_RELU: return dispatch_glds<DT, EPI_BIAS_RELU>(b, cfg, s, nb);
+  }
+  return -6;
+}
+
 // 3x3 / 1x1 conv + bias + ReLU with the 2x2/s2 max-pool fused into the epilogue: yp = pooled output,
 // codes = its max-pool codes (what the backward needs), y = the full-resolution output (optional: nullptr
 // skips its 2-byte-per-element store).  LDS-DMA v2 kernels and conv1_2's halo kernel.
@@ -1674,6 +1706,13 @@ extern "C" int can_conv_igemm(const void* x, const void* w, const float* bias, c
                               int* bpart_rows) {
   CAN_DT_DISPATCH(dt, can::conv_igemm_impl<DT>(x, w, bias, mask, y, N, H, W, Cin, Cout, ksize, dil, epi, first,
                                               tile_cfg, stream, bpart, bpart_cap, bpart_rows));
+}
+
+extern "C" int can_conv_igemm_batched(const void* x, const void* w, const float* bias, void* y, int nb, long long xbs,
+                                      long long wbs, long long ybs, int N, int H, int W, int Cin, int Cout, int ksize,
+                                      int dil, int epi, int tile_cfg, int dt, void* stream) {
+  CAN_DT_DISPATCH(dt, can::conv_igemm_batched_impl<DT>(x, w, bias, y, nb, xbs, wbs, ybs, N, H, W, Cin, Cout, ksize, dil,
+                                                      epi, tile_cfg, (hipStream_t)stream));
 }
 
 extern "C" int can_conv_pool_fwd(const void* x, const void* w, const float* bias, void* y, void* yp, void* codes,

@@ -141,6 +141,37 @@ def conv_igemm(x: torch.Tensor, wpack: torch.Tensor, bias: Optional[torch.Tensor
     return out
 
 
+def conv_igemm_batched(x: torch.Tensor, wpack: torch.Tensor, *, ksize: int, epi: int, dil: int = 1,
+                       out: Optional[torch.Tensor] = None, tile: int = 0) -> torch.Tensor:
+    """nb independent convs of one shape in one launch: x [nb,N,H,W,Ci], wpack [nb,Co,K] -> [nb,N,H,W,Co];
+    epi EPI_NONE or EPI_SIGMOID (no bias).  Same kernel and tile config as nb conv_igemm calls (bitwise)."""
+    C = _ext.require()
+    if x.dim() != 5 or wpack.dim() != 3 or x.shape[0] != wpack.shape[0]:
+        raise ValueError("x must be [nb,N,H,W,C] and wpack [nb,Co,K] with the same nb")
+    if epi not in (EPI_NONE, EPI_SIGMOID):
+        raise ValueError("batched convs take EPI_NONE or EPI_SIGMOID")
+    nb, n, h, w, ci = x.shape
+    _check_act(x, "x")
+    _, co, k = wpack.shape
+    if wpack.dtype != x.dtype or not wpack.is_contiguous():
+        raise ValueError(f"wpack must be contiguous {x.dtype}")
+    if ci % 64 or co % 64 or k != ksize * ksize * ci or ksize not in (1, 3):
+        raise ValueError("Cin / Cout must be multiples of 64 and K = ksize^2 * Cin")
+    if h < 2 or w < 2:
+        raise ValueError("H and W must be >= 2")
+    oshape = (nb, n, h, w, co)
+    if out is None:
+        out = torch.empty(*oshape, dtype=x.dtype, device=x.device)
+    elif tuple(out.shape) != oshape:
+        raise ValueError("out has the wrong shape")
+    else:
+        _check_act(out, "out", dtype=x.dtype)
+    C.conv_igemm_batched(x.data_ptr(), wpack.data_ptr(), 0, out.data_ptr(), nb, n * h * w * ci, co * k,
+                         n * h * w * co, n, h, w, ci, co, ksize, dil, epi, tile, dt_code(x.dtype),
+                         _ext.stream_ptr(x.device))
+    return out
+
+
 BIAS_ROWS = 512     # bias partial rows the weight-gradient reduce kernels take directly (kBiasParts)
 
 

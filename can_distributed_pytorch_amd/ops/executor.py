@@ -124,10 +124,11 @@ class CANNetExecutor:
                 fwd = torch.empty(s.cout, s.ksize * s.ksize * s.cin, dtype=self.act, device=device)
                 dgr = torch.empty(s.cin, s.ksize * s.ksize * s.cout, dtype=self.act, device=device)
             self.packs[id(w)] = (fwd, dgr)
-        for sc in CONTEXT_SCALES:
-            w = self.ctx2[sc].weight
-            self.packs[id(w)] = (torch.empty(512, 512, dtype=self.act, device=device),
-                                 torch.empty(512, 512, dtype=self.act, device=device))
+        # the four conv{S}_2 packs are items of one [4, 512, 512] buffer each (one batched launch per pass)
+        self.ctx2_fwd = torch.empty(len(CONTEXT_SCALES), 512, 512, dtype=self.act, device=device)
+        self.ctx2_dgr = torch.empty_like(self.ctx2_fwd)
+        for i, sc in enumerate(CONTEXT_SCALES):
+            self.packs[id(self.ctx2[sc].weight)] = (self.ctx2_fwd[i], self.ctx2_dgr[i])
 
     def refresh_packs(self, force: bool = False):
         """Re-pack the 16-bit weight copies from the fp32 masters (one launch for all layers)."""
@@ -291,13 +292,21 @@ class CANNetExecutor:
         cs = torch.empty(4, n, h, w, c, dtype=self.act, device=fv.device)
         self.C.ctx_expand(fv.data_ptr(), table.data_ptr(), cs.data_ptr(), n, h, w, c, self.dt, st)
         wts = torch.empty(4, n, h, w, c, dtype=self.act, device=fv.device)
-        for i, sc in enumerate(CONTEXT_SCALES):
-            fwd, _ = self.packs[id(self.ctx2[sc].weight)]
-            C.conv_igemm(cs[i], fwd, None, ksize=1, epi=4, out=wts[i])   # EPI_SIGMOID
+        if self._ctx_batched(h, w):
+            C.conv_igemm_batched(cs, self.ctx2_fwd, ksize=1, epi=C.EPI_SIGMOID, out=wts)   # one launch
+        else:
+            for i, sc in enumerate(CONTEXT_SCALES):
+                fwd, _ = self.packs[id(self.ctx2[sc].weight)]
+                C.conv_igemm(cs[i], fwd, None, ksize=1, epi=C.EPI_SIGMOID, out=wts[i])
         cat = torch.empty(n, h, w, 2 * c, dtype=self.act, device=fv.device)
         self.C.ctx_fuse(fv.data_ptr(), wts.data_ptr(), table.data_ptr(), cat.data_ptr(), n, h, w, c, self.dt, st)
         saved = dict(ave=ave, table=table, cs=cs, wts=wts, rowacc=rowacc) if save else None
         return cat, saved
+
+    @staticmethod
+    def _ctx_batched(h, w):
+        """The four conv{S}_2 1x1 convs as one batched launch (CANNET_CTX_BATCHED=0: four launches)."""
+        return h >= 2 and w >= 2 and os.environ.get("CANNET_CTX_BATCHED", "1") != "0"
 
     def _ctx1_ptrs(self):
         ws = [self.ctx1[sc].weight for sc in CONTEXT_SCALES]
@@ -437,9 +446,12 @@ class CANNetExecutor:
         self.C.ctx_bwd_e1(dcat.data_ptr(), ctx["wts"].data_ptr(), ctx["table"].data_ptr(), dz.data_ptr(),
                           sdir.data_ptr(), n, h, w, c, self.dt, st)
         dc = torch.empty_like(dz)
-        for i, sc in enumerate(CONTEXT_SCALES):
-            _, dgr = self.packs[id(self.ctx2[sc].weight)]
-            C.conv_igemm(dz[i], dgr, None, ksize=1, epi=C.EPI_NONE, out=dc[i])
+        if self._ctx_batched(h, w):
+            C.conv_igemm_batched(dz, self.ctx2_dgr, ksize=1, epi=C.EPI_NONE, out=dc)
+        else:
+            for i, sc in enumerate(CONTEXT_SCALES):
+                _, dgr = self.packs[id(self.ctx2[sc].weight)]
+                C.conv_igemm(dz[i], dgr, None, ksize=1, epi=C.EPI_NONE, out=dc[i])
         # the four conv{S}_2 weight gradients: one batched GEMM when their arena slots are adjacent
         dws = [grads[self.ctx2_index[sc]] for sc in CONTEXT_SCALES]
 

@@ -411,3 +411,18 @@ def test_ws64_matches_halo_kernel(n, h, w, epi, monkeypatch):
         xr = torch.zeros(n, 64, h, w, device=dev, requires_grad=True)
         (gx,) = torch.autograd.grad(F.conv2d(xr, wt, None, padding=1), xr, x.float().permute(0, 3, 1, 2))
         _close(new[0], gx.permute(0, 2, 3, 1) * (mask.float() > 0))
+
+
+@pytest.mark.parametrize("epi", [2, 4])
+@pytest.mark.parametrize("n,h,w,ci,co,k", [(2, 12, 16, 512, 512, 1), (1, 9, 13, 128, 256, 3)])
+def test_conv_igemm_batched_matches_per_item(n, h, w, ci, co, k, epi):
+    """nb convs in one launch (grid.y = item) == nb single launches, bitwise (context module conv{S}_2)."""
+    from can_distributed_pytorch_amd.ops import conv as C
+    torch.manual_seed(15)
+    nb = 4
+    x = torch.randn(nb, n, h, w, ci, device="cuda").to(torch.bfloat16)
+    wp = torch.stack([C.pack_weight_fwd(torch.randn(co, ci, k, k, device="cuda") * 0.05) for _ in range(nb)])
+    y = C.conv_igemm_batched(x, wp, ksize=k, epi=epi)
+    ref = torch.stack([C.conv_igemm(x[i], wp[i], None, ksize=k, epi=epi) for i in range(nb)])
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
