@@ -166,12 +166,29 @@ __global__ void __launch_bounds__(256) ctx_cells_kernel(const float* __restrict_
     const int local = cell - kCellOff[si];
     const int i = local / S, j = local % S;
     const int bin = kBinOff[si] + j;
-    float s = 0.f;
-    for (int y = 0; y < h; ++y) {
-      const float wt = axis_w<POOL>(i, S, y, h);
-      if (wt != 0.f) s += wt * rowacc[(((size_t)n * h + y) * 12 + bin) * C + c];
+    // rows y where the cell-row weight can be non-zero (a superset: axis_w is exact), then 4 independent
+    // partial sums so the loads of 4 rows are in flight together (fixed order: deterministic)
+    int y_lo = 0, y_hi = h;
+    if (POOL) {
+      pool_bin(i, S, h, y_lo, y_hi);
+    } else if (S > 1) {
+      y_lo = max(0, ((i - 1) * (h - 1)) / (S - 1) - 1);
+      y_hi = min(h, ((i + 1) * (h - 1)) / (S - 1) + 2);
     }
-    cells[t] = s;
+    const float* col = rowacc + ((size_t)n * h * 12 + bin) * C + c;
+    const size_t ystride = (size_t)12 * C;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int y = y_lo;
+    for (; y + 3 < y_hi; y += 4) {
+      const float v0 = col[(size_t)y * ystride], v1 = col[(size_t)(y + 1) * ystride];
+      const float v2 = col[(size_t)(y + 2) * ystride], v3 = col[(size_t)(y + 3) * ystride];
+      s0 += axis_w<POOL>(i, S, y, h) * v0;
+      s1 += axis_w<POOL>(i, S, y + 1, h) * v1;
+      s2 += axis_w<POOL>(i, S, y + 2, h) * v2;
+      s3 += axis_w<POOL>(i, S, y + 3, h) * v3;
+    }
+    for (; y < y_hi; ++y) s0 += axis_w<POOL>(i, S, y, h) * col[(size_t)y * ystride];
+    cells[t] = (s0 + s1) + (s2 + s3);
   }
 }
 

@@ -53,7 +53,7 @@ def _ctx_ref(fv, w1, w2):
     return torch.cat((fv, num / (den + 1e-12)), 1)
 
 
-@pytest.mark.parametrize("n,h,w", [(2, 12, 16), (1, 13, 22)])
+@pytest.mark.parametrize("n,h,w", [(2, 12, 16), (1, 13, 22), (2, 96, 128), (1, 67, 45)])
 def test_context_fwd_bwd(n, h, w):
     from can_distributed_pytorch_amd.models import CANNet
     from can_distributed_pytorch_amd.ops.executor import CANNetExecutor
