@@ -289,26 +289,58 @@ __global__ void __launch_bounds__(256) grad_nonfinite_kernel(const float4* __res
 // block b = lo if bit b of `pattern` is set, else hi:
 //   mode 0 (K-concatenated operand): dst [M][stride], block b at channels [b*C, (b+1)*C), zero from 3*C on;
 //   mode 1 (M-stacked operand):      dst [3][M][stride], block b = rows [b*M, (b+1)*M), zero from C on.
-__global__ void __launch_bounds__(256) split_x3_kernel(const float* __restrict__ src, unsigned short* __restrict__ dst,
-                                                       long long M, int C, int stride, int mode, int pattern) {
-  const long long total = (mode == 0 ? 1 : 3) * M * (long long)stride;
-  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const long long row = i / stride;
-    const int col = (int)(i - row * stride);
-    int b, c;
-    long long m;
-    if (mode == 0) {
-      m = row; b = col / C; c = col - b * C;
-    } else {
-      b = (int)(row / M); m = row - (long long)b * M; c = col;
+// General form (small or padded C, e.g. the 3-channel image into 64-channel rows): one thread per output row
+// chunk of 8 values (one 16-byte store; stride % 8 == 0).
+__global__ void __launch_bounds__(256) split_x3_kernel(const float* __restrict__ src, uint4* __restrict__ dst,
+                                                       int M, int C, int stride, int mode, int pattern) {
+  const int rows = (mode == 0 ? 1 : 3) * M, s8 = stride >> 3;
+  const long long total = (long long)rows * s8;
+  for (long long t = blockIdx.x * 256ll + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const int row = (int)(t / s8), col0 = (int)(t - (long long)row * s8) * 8;
+    const int b0 = (mode == 0) ? 0 : row / M;
+    const int m = (mode == 0) ? row : row - b0 * M;
+    unsigned short v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int col = col0 + k;
+      const int b = (mode == 0) ? col / C : b0;
+      const int c = (mode == 0) ? col - b * C : col;
+      unsigned short o = 0;
+      if (b < 3 && c < C) {
+        const float x = src[(size_t)m * C + c];
+        const unsigned short hi = f2bf(x);
+        o = ((pattern >> b) & 1) ? f2bf(x - bf2f(hi)) : hi;
+      }
+      v[k] = o;
     }
-    unsigned short v = 0;
-    if (b < 3 && c < C) {
-      const float x = src[m * C + c];
-      const unsigned short hi = f2bf(x);
-      v = ((pattern >> b) & 1) ? f2bf(x - bf2f(hi)) : hi;
+    dst[t] = make_uint4(v[0] | ((unsigned)v[1] << 16), v[2] | ((unsigned)v[3] << 16), v[4] | ((unsigned)v[5] << 16),
+                        v[6] | ((unsigned)v[7] << 16));
+  }
+}
+
+// Fast path (C % 4 == 0, no padding columns): one thread per 4 source values; one float4 read, three 8-byte
+// stores, 32-bit index math (the generic kernel's 64-bit divisions made it 30 % of the fp32 step).
+__global__ void __launch_bounds__(256) split_x3_vec_kernel(const float4* __restrict__ src, uint2* __restrict__ dst,
+                                                           int M, int C4, int mode, int pattern) {
+  const int total = M * C4;
+  for (int t = blockIdx.x * 256 + threadIdx.x; t < total; t += gridDim.x * 256) {
+    const float4 x = src[t];
+    const float xv[4] = {x.x, x.y, x.z, x.w};
+    unsigned short hi[4], lo[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      hi[k] = f2bf(xv[k]);
+      lo[k] = f2bf(xv[k] - bf2f(hi[k]));
     }
-    dst[i] = v;
+    const uint2 h = make_uint2(hi[0] | ((unsigned)hi[1] << 16), hi[2] | ((unsigned)hi[3] << 16));
+    const uint2 l = make_uint2(lo[0] | ((unsigned)lo[1] << 16), lo[2] | ((unsigned)lo[3] << 16));
+    const int m = t / C4, c4 = t - m * C4;
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      const uint2 v = ((pattern >> b) & 1) ? l : h;
+      if (mode == 0) dst[(size_t)m * 3 * C4 + b * C4 + c4] = v;      // [M][3C]
+      else dst[(size_t)b * total + t] = v;                           // [3][M][C]
+    }
   }
 }
 
@@ -490,8 +522,16 @@ extern "C" int can_split_x3(const float* src, void* dst, long long M, int C, int
                             void* stream) {
   if (M < 1 || C < 1 || (mode == 0 && stride < 3 * C) || (mode == 1 && stride < C) || mode < 0 || mode > 1) return -2;
   const size_t total = (size_t)(mode == 0 ? 1 : 3) * (size_t)M * (size_t)stride;
-  hipLaunchKernelGGL(split_x3_kernel, dim3(grid_for(total, 256, 8192)), dim3(256), 0, (hipStream_t)stream, src,
-                     (unsigned short*)dst, M, C, stride, mode, pattern);
+  const bool dense = (mode == 0) ? stride == 3 * C : stride == C;
+  if (dense && C % 4 == 0 && (size_t)M * C < (1u << 31) && ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 7) == 0) {
+    const size_t n4 = (size_t)M * (C / 4);
+    hipLaunchKernelGGL(split_x3_vec_kernel, dim3(grid_for(n4, 256, 16384)), dim3(256), 0, (hipStream_t)stream,
+                       (const float4*)src, (uint2*)dst, (int)M, C / 4, mode, pattern);
+    return (int)hipGetLastError();
+  }
+  if (stride % 8 || (size_t)M * 3 >= (1u << 31) || ((uintptr_t)dst & 15)) return -3;
+  hipLaunchKernelGGL(split_x3_kernel, dim3(grid_for(total / 8, 256, 16384)), dim3(256), 0, (hipStream_t)stream, src,
+                     (uint4*)dst, (int)M, C, stride, mode, pattern);
   return (int)hipGetLastError();
 }
 

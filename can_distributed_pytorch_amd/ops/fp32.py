@@ -208,6 +208,53 @@ def _run_seq(seq, y):
     return y
 
 
+_AXIS_CACHE = {}
+
+
+def _pool_matrix(S: int, L: int, device) -> torch.Tensor:
+    """[S, L] adaptive-average-pool weights (ATen bins: floor(i*L/S) .. ceil((i+1)*L/S))."""
+    key = ("pool", S, L, str(device))
+    if key not in _AXIS_CACHE:
+        m = torch.zeros(S, L, dtype=torch.float64)
+        for i in range(S):
+            st, en = (i * L) // S, -(-((i + 1) * L) // S)
+            m[i, st:en] = 1.0 / (en - st)
+        _AXIS_CACHE[key] = m.float().to(device)
+    return _AXIS_CACHE[key]
+
+
+def _interp_matrix(S: int, L: int, device) -> torch.Tensor:
+    """[L, S] bilinear (align_corners=True) weights of output position x over the S input cells."""
+    key = ("up", S, L, str(device))
+    if key not in _AXIS_CACHE:
+        m = torch.zeros(L, S, dtype=torch.float64)
+        scale = (S - 1) / (L - 1) if L > 1 else 0.0
+        for x in range(L):
+            src = scale * x
+            x0 = int(src)
+            x1 = x0 + (1 if x0 < S - 1 else 0)
+            lam = src - x0
+            m[x, x0] += 1.0 - lam
+            m[x, x1] += lam
+        _AXIS_CACHE[key] = m.float().to(device)
+    return _AXIS_CACHE[key]
+
+
+def _adaptive_pool_nhwc(x: torch.Tensor, S: int) -> torch.Tensor:
+    """adaptive_avg_pool2d on NHWC as two fp32 GEMMs (their backward is GEMMs too); ATen's NHWC kernels for a
+    96 x 128 -> 1..6 pooling and its bilinear backward took 17 ms of the fp32 step."""
+    n, h, w, c = x.shape
+    t = torch.matmul(_pool_matrix(S, w, x.device), x)                       # [n, h, S, c]
+    return torch.matmul(_pool_matrix(S, h, x.device), t.reshape(n, h, S * c)).reshape(n, S, S, c)
+
+
+def _upsample_nhwc(a: torch.Tensor, h: int, w: int) -> torch.Tensor:
+    """bilinear upsample (align_corners=True) of NHWC [n, S, S, c] to [n, h, w, c] as two fp32 GEMMs."""
+    n, S, _, c = a.shape
+    t = torch.matmul(_interp_matrix(S, w, a.device), a)                     # [n, S, w, c]
+    return torch.matmul(_interp_matrix(S, h, a.device), t.reshape(n, S, w * c)).reshape(n, h, w, c)
+
+
 def cannet_forward_fp32(model, img: torch.Tensor) -> torch.Tensor:
     """CANNet forward (model/CANNet.py:39-91 math) with every convolution on conv2d_x3; img [N,3,H,W] fp32 ->
     density [N,1,H/8,W/8] fp32."""
@@ -216,11 +263,10 @@ def cannet_forward_fp32(model, img: torch.Tensor) -> torch.Tensor:
     fv = _run_seq(model.frontend, x)                             # [N,h,w,512]
     n, h, w, c = fv.shape
     num = den = None
-    fvc = _nchw(fv)
     for s in CONTEXT_SCALES:
         c1, c2 = getattr(model, f"conv{s}_1"), getattr(model, f"conv{s}_2")
-        ave = conv2d_x3(_nhwc(F.adaptive_avg_pool2d(fvc, (s, s))), c1.weight, None)
-        up = _nhwc(F.interpolate(_nchw(ave), size=(h, w), mode="bilinear", align_corners=True))
+        ave = conv2d_x3(_adaptive_pool_nhwc(fv, s), c1.weight, None)
+        up = _upsample_nhwc(ave, h, w)
         wgt = torch.sigmoid(conv2d_x3(up - fv, c2.weight, None))
         num = wgt * up if num is None else num + wgt * up
         den = wgt if den is None else den + wgt
