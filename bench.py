@@ -57,6 +57,8 @@ def parse(argv=None):
     p.add_argument("--graph", type=int, default=0,
                    help="hipGraph-capture the step (hip impl).  Off by default: see profiles/README.md (graph)")
     p.add_argument("--comm-steps", type=int, default=3, help="extra untimed steps with all-reduce timing events")
+    p.add_argument("--mode", choices=["train", "infer"], default="train",
+                   help="train: the headline training step; infer: forward-only density estimation (serving)")
     return p.parse_args(argv)
 
 
@@ -81,6 +83,49 @@ def launch_ranks(a) -> int:
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return subprocess.run(cmd, env=env).returncode
+
+
+def infer(a, trainer, pool, sync_all, world, rank, local, dev) -> int:
+    """Forward-only throughput (test.py's density estimation): eval mode, no autograd, the same kernels as the
+    training forward (native: executor.forward_eval + the 1x1 head)."""
+    import torch
+    import torch.distributed as dist
+    model = trainer.model
+    model.eval()
+    cast = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(a.dtype) if a.impl == "torch" else None
+    imgs = [p[0] for p in pool]
+
+    def fwd(x):
+        with torch.no_grad():
+            if cast is not None:
+                with torch.autocast("cuda", dtype=cast):
+                    return model(x.contiguous(memory_format=torch.channels_last))
+            return model(x)
+    for i in range(a.warmup):
+        fwd(imgs[i % len(imgs)])
+    sync_all()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        et = fwd(imgs[i % len(imgs)])
+    sync_all()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    if rank == 0:
+        print(json.dumps({
+            "metric": "CANNet inference imgs/sec (forward only, density map)", "value": round(a.batch * world * a.steps / dt, 3),
+            "unit": "imgs/sec", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(1000.0 * dt / a.steps, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": a.dtype, "data": "synthetic",
+            "config": {"model": "CANNet", "global_batch": a.batch * world, "per_gpu_batch": a.batch,
+                       "image_hw": [a.height, a.width], "impl": a.impl, "mode": "infer"},
+            "count_first_image": float(et[0].sum())}), flush=True)
+    if world > 1:
+        dist.barrier(device_ids=[local])
+        dist.destroy_process_group()
+    return 0
 
 
 def main(argv=None) -> int:
@@ -117,6 +162,9 @@ def main(argv=None) -> int:
         if world > 1:
             dist.barrier(device_ids=[local])
         torch.cuda.synchronize()
+
+    if a.mode == "infer":
+        return infer(a, trainer, pool, sync_all, world, rank, local, dev)
 
     for i in range(a.warmup):
         trainer.step(*pool[i % len(pool)])

@@ -27,3 +27,14 @@ def test_world_size_mismatch_fails_loudly():
     r = _run(["--gpus", "2", "--steps", "1", "--warmup", "0"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 2, (r.returncode, r.stdout, r.stderr)
     assert "WORLD_SIZE=1" in r.stderr and r.stdout.strip() == ""
+
+
+def test_mode_flag_defaults_to_training():
+    """The driver's contract line is the training step; --mode infer is an opt-in serving measurement."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(os.path.dirname(__file__), "..", "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert bench.parse([]).mode == "train"
+    assert bench.parse(["--mode", "infer"]).mode == "infer"
