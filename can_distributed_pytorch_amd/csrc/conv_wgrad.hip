@@ -634,6 +634,9 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
     return sa;
   };
   auto issue_part = [&](const StageAddr& sa, int p, int parts) {
+#if defined(CAN_WPROBE) && (CAN_WPROBE & 1)
+    return;                                         // diagnostic build (scripts/probe): no DMA
+#endif
 #pragma unroll
     for (int j = p * GA / parts; j < (p + 1) * GA / parts; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(dy_rsrc, (__attribute__((address_space(3))) void*)(sa.sbase + (wave + NW * j) * 1024),
@@ -657,6 +660,9 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
 
   const int g = lane >> 4, qd = (lane & 15) >> 2, p = lane & 3;
   auto rd = [&](const unsigned char* base, int rb_wide, int rb, int prow0, int col0) -> frag8_t {
+#if defined(CAN_WPROBE) && (CAN_WPROBE & 2)
+    return __builtin_bit_cast(frag8_t, make_uint4(prow0 + lane, col0, rb, 1));   // diagnostic: no LDS reads
+#endif
     const int r0 = prow0 + 8 * g + qd;
     const int c8 = (col0 >> 2) + p;
     const int s0 = rb_wide ? swz8b<256>(r0, c8) : swz8b<128>(r0, c8);
