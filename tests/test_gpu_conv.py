@@ -171,6 +171,35 @@ def test_conv_wgrad_halo_path(n, h, w, ci, co, ring, monkeypatch):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("n,h,w,ci,co", [(2, 128, 1024, 64, 64), (1, 512, 576, 128, 128), (4, 96, 704, 64, 128)])
+def test_ring_wgrad_fast_addressing_bitwise(n, h, w, ci, co, dtype, monkeypatch):
+    """Row-ring weight gradient with the hoisted DMA addressing (H % 4 == 0, W % 64 == 0: per-lane offsets from the
+    tile / row origins, edge slots zeroed per lane) == the general per-piece addressing (CANNET_RING_FAST=0),
+    bitwise: several strips per image, several images, 2 ci / co tiles, slices crossing strips."""
+    from can_distributed_pytorch_amd.ops import _ext
+    from can_distributed_pytorch_amd.ops import conv as C
+    assert _ext.require().wgrad_plan(n * h * w, ci, co, 3, 0, 1024)[2] == 8
+    torch.manual_seed(21)
+    x = torch.randn(n, h, w, ci, device="cuda").to(dtype)
+    dy = torch.randn(n, h, w, co, device="cuda").to(dtype)
+    dw0, db0 = torch.empty(co, ci, 3, 3, device="cuda"), torch.empty(co, device="cuda")
+    dw1, db1 = torch.empty_like(dw0), torch.empty_like(db0)
+    ws = C.WgradWorkspace("cuda")
+    C.conv_wgrad(dy, x, dw0, db0, ksize=3, dil=1, ws=ws)
+    monkeypatch.setenv("CANNET_RING_FAST", "0")
+    C.conv_wgrad(dy, x, dw1, db1, ksize=3, dil=1, ws=ws)
+    torch.cuda.synchronize()
+    assert torch.equal(dw0, dw1) and torch.equal(db0, db1)
+    if n * h * w <= 300000:
+        wr = torch.zeros(co, ci, 3, 3, device="cuda", requires_grad=True)
+        br = torch.zeros(co, device="cuda", requires_grad=True)
+        y = F.conv2d(x.float().permute(0, 3, 1, 2), wr, br, padding=1)
+        gw, gb = torch.autograd.grad(y, (wr, br), dy.float().permute(0, 3, 1, 2))
+        _close(dw0, gw, 1e-2)
+        _close(db0, gb, 1e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 def test_conv_wgrad_1x1_batched(dtype):
     """The four context-module 1x1 weight gradients in one batched launch == fp32 reference, per item."""
     from can_distributed_pytorch_amd.ops import conv as C
