@@ -627,7 +627,12 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
     aoff[j] = (ct * TC + perm_row(r)) * Ktot + lc8;
   }
   int boff[GB];
-  unsigned bmask[GB];
+  // 9-bit tap-validity masks, three per VGPR (the 128 x 512 tile's 8 pieces per wave otherwise push the
+  // kernel past 256 VGPRs into scratch)
+  constexpr int NBM = (GB + 2) / 3;
+  unsigned bmask[NBM];
+#pragma unroll
+  for (int j = 0; j < NBM; ++j) bmask[j] = 0u;
 #pragma unroll
   for (int j = 0; j < GB; ++j) {
     const int r = (wave + NW * j) * 8 + (lane >> 3);
@@ -648,7 +653,7 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
       }
     }
     boff[j] = m * a.Cin + lc8;
-    bmask[j] = msk;
+    bmask[j / 3] |= msk << (9 * (j % 3));
   }
 
   // stage -> (channel chunk, tap) advanced incrementally (scalar).  Stages run
@@ -676,7 +681,7 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
       __builtin_amdgcn_global_load_lds((const void*)(a.w + aoff[j] + i_k), (__attribute__((address_space(3))) void*)(sbase + (wave + NW * j) * 1024), 16, 0, 0);
 #pragma unroll
     for (int j = p * GB / PARTS; j < (p + 1) * GB / PARTS; ++j) {
-      const void* src = ((bmask[j] >> i_tap) & 1u) ? (const void*)(a.x + boff[j] + sh) : (const void*)a.zero;
+      const void* src = ((bmask[j / 3] >> (9 * (j % 3) + i_tap)) & 1u) ? (const void*)(a.x + boff[j] + sh) : (const void*)a.zero;
       __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sbase + A_BYTES + (wave + NW * j) * 1024), 16, 0, 0);
     }
     if (p == PARTS - 1 && ++i_tap == ntap) { i_tap = 0; i_c0 += 64; }
@@ -703,7 +708,7 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
 #endif
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
-      const void* src = ((bmask[j] >> i_tap) & 1u) ? (const void*)(a.x + boff[j] + sh) : (const void*)a.zero;
+      const void* src = ((bmask[j / 3] >> (9 * (j % 3) + i_tap)) & 1u) ? (const void*)(a.x + boff[j] + sh) : (const void*)a.zero;
       __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sbase + A_BYTES + (wave + NW * j) * 1024), 16, 0, 0);
     }
     if (++i_tap == ntap) { i_tap = 0; i_c0 += 64; }
@@ -1159,8 +1164,12 @@ conv_halo64_kernel(HaloConvArgs a) {
 // ===========================================================================
 template <int DT, int EPI>
 __global__ void __launch_bounds__(512, 1) conv_ws64_kernel(HaloConvArgs a) {
-  constexpr int TR = 4, TCOL = 64, HC = TCOL + 2, HPIX = (TR + 2) * HC;   // 396 halo pixels
-  constexpr int NHI = (HPIX + 7) / 8;                                      // 50 one-KiB DMA pieces
+  // halo rows of 66 pixels stored at a 72-pixel stride: a 1-KiB DMA piece (8 pixels) never straddles two
+  // rows, so wave w fetches piece column w of all 6 rows (pixel slot 8w + lane / 8, a per-lane constant)
+  // and waves 0-5 the 9th column (slots 64, 65 + padding) of row w: per piece one address add and one
+  // column bounds compare, the row bounds are scalar (was: a division by 66 and a 64-bit multiply per piece)
+  constexpr int TR = 4, TCOL = 64, HC = TCOL + 2, HCP = 72;
+  constexpr int NHI = (TR + 2) * (HCP / 8);                                // 54 one-KiB DMA pieces
   constexpr int HALO_BYTES = NHI * 1024;
   static_assert(EPI == EPI_BIAS_RELU || EPI == EPI_BIAS || EPI == EPI_NONE || EPI == EPI_MASK ||
                 EPI == EPI_POOLFWD, "ws64 epilogues");
@@ -1188,14 +1197,25 @@ __global__ void __launch_bounds__(512, 1) conv_ws64_kernel(HaloConvArgs a) {
   auto issue_halo = [&](int t, unsigned char* buf) {
     int n, oh0, ow0;
     tile_org(t, n, oh0, ow0);
-    for (int i = wave; i < NHI; i += 8) {
-      const int hp = i * 8 + (lane >> 3);
-      const int hr = hp / HC, hc = hp - hr * HC;
-      const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
-      const void* src = a.zero;
-      if (hp < HPIX && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
-        src = a.x + ((size_t)(n * a.H + ih) * a.W + iw) * 64 + (((lane & 7) ^ (hc & 7)) * 8);
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(buf + i * 1024), 16, 0, 0);
+    int ln = lane;
+    asm volatile("" : "+v"(ln));                    // per-lane math stays here (the kernel is at its VGPR cap)
+    const int c0 = wave * 8 + (ln >> 3), c1 = 64 + (ln >> 3);          // slots of piece column wave / 8
+    const int o0 = c0 * 64 + (((ln & 7) ^ (c0 & 7)) * 8), o1 = c1 * 64 + (((ln & 7) ^ (c1 & 7)) * 8);
+    const bool v0 = (unsigned)(ow0 - 1 + c0) < (unsigned)a.W;
+    const bool v1 = c1 < HC && (unsigned)(ow0 - 1 + c1) < (unsigned)a.W;
+#pragma unroll
+    for (int hr = 0; hr < TR + 2; ++hr) {
+      const int ih = oh0 - 1 + hr;
+      const bool row_in = ih >= 0 && ih < a.H;      // wave-uniform
+      const bf16_t* rbase = a.x + ((ptrdiff_t)(n * a.H + ih) * a.W + ow0 - 1) * 64;
+      const void* src = (row_in && v0) ? (const void*)(rbase + o0) : (const void*)a.zero;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(buf + (hr * 9 + wave) * 1024),
+                                       16, 0, 0);
+      if (wave == hr) {                             // the 9th piece column: one row per wave 0 .. 5
+        const void* src1 = (row_in && v1) ? (const void*)(rbase + o1) : (const void*)a.zero;
+        __builtin_amdgcn_global_load_lds(src1, (__attribute__((address_space(3))) void*)(buf + (hr * 9 + 8) * 1024),
+                                         16, 0, 0);
+      }
     }
   };
 
@@ -1226,7 +1246,7 @@ __global__ void __launch_bounds__(512, 1) conv_ws64_kernel(HaloConvArgs a) {
   for (int kw = 0; kw < 3; ++kw)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
-      hoff[kw][kk] = (r * HC + fr + kw) * 128 + (((kk * 4 + fq) ^ ((fr + kw) & 7)) * 16);
+      hoff[kw][kk] = (r * HCP + fr + kw) * 128 + (((kk * 4 + fq) ^ ((fr + kw) & 7)) * 16);
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
 
   for (int t = t0, it = 0; t < t1; ++t, ++it) {
@@ -1257,7 +1277,7 @@ __global__ void __launch_bounds__(512, 1) conv_ws64_kernel(HaloConvArgs a) {
       frag8_t bfr[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        bfr[i] = __builtin_bit_cast(frag8_t, *reinterpret_cast<const uint4*>(cur + hoff[kw][kk] + kh * HC * 128 +
+        bfr[i] = __builtin_bit_cast(frag8_t, *reinterpret_cast<const uint4*>(cur + hoff[kw][kk] + kh * HCP * 128 +
                                                                               i * 2048));
 #pragma unroll
       for (int j = 0; j < 2; ++j)
@@ -1328,7 +1348,7 @@ __global__ void __launch_bounds__(512, 1) conv_ws64_kernel(HaloConvArgs a) {
 
 template <int DT, int EPI>
 static int launch_ws64(const HaloConvArgs& a, hipStream_t s) {
-  constexpr size_t lds = 2 * (size_t)(((6 * 66) + 7) / 8) * 1024;
+  constexpr size_t lds = 2 * (size_t)(6 * 9) * 1024;       // 2 halo buffers of 6 rows x 72 pixel slots
   auto kfn = conv_ws64_kernel<DT, EPI>;
   static int ncu = 0;
   if (!ncu) {
