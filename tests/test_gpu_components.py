@@ -261,3 +261,44 @@ def test_gpu_preprocess_matches_cpu_transform():
             assert np.abs(got - ref_img).max() < 0.03          # bf16 storage of the normalised image
             assert bool((x4[0, ..., 3] == 0).all())
             assert np.abs(gt[0].cpu().numpy() - ref_gt).max() < 1e-3
+
+
+@pytest.mark.parametrize("arena", [False, True])
+def test_weight_packs_bitwise(arena):
+    """One-launch weight packing (pack_multi: 16-B vector path for whole 32x32 tiles, element-wise otherwise) ==
+    the Python packs of every layer, bitwise; arena=True: fp32 masters that are not 16-B aligned (element-wise
+    loads, vector stores)."""
+    from can_distributed_pytorch_amd.models import CANNet
+    from can_distributed_pytorch_amd.ops import conv as C
+    from can_distributed_pytorch_amd.ops.executor import CANNetExecutor
+    torch.manual_seed(3)
+    model = CANNet().cuda()
+    for p in model.parameters():
+        torch.nn.init.normal_(p, std=0.3)
+    if arena:
+        # masters as views at a 1-float offset of one buffer: no slot 16-B aligned -> element-wise loads
+        ps = list(model.parameters())
+        buf = torch.zeros(1 + sum(p.numel() for p in ps), device="cuda")
+        off = 1
+        with torch.no_grad():
+            for p in ps:
+                n = p.numel()
+                buf[off:off + n].copy_(p.reshape(-1))
+                p.data = buf[off:off + n].view_as(p)
+                off += n
+        assert any(p.data_ptr() % 16 for p in ps if p.dim() == 4 and p.shape[1] >= 64)
+    ex = CANNetExecutor(model)
+    ex.refresh_packs(force=True)
+    torch.cuda.synchronize()
+    for s in ex.front + ex.back:
+        fwd, dgr = ex.packs[id(s.module.weight)]
+        w = s.module.weight
+        if s.first:
+            assert torch.equal(fwd, C.pack_weight_first(w))
+            continue
+        assert torch.equal(fwd, C.pack_weight_fwd(w)), s.idx
+        assert torch.equal(dgr, C.pack_weight_dgrad(w)), s.idx
+    for sc in (1, 2, 3, 6):
+        fwd, dgr = ex.packs[id(ex.ctx2[sc].weight)]
+        assert torch.equal(fwd, C.pack_weight_fwd(ex.ctx2[sc].weight))
+        assert torch.equal(dgr, C.pack_weight_dgrad(ex.ctx2[sc].weight))
