@@ -16,6 +16,7 @@ Weight layouts (packed from the fp32 master weights [Co][Ci][kh][kw]):
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -309,8 +310,19 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, db: Optional
                  _ext.stream_ptr(x.device), bx, brows)
 
 
-def wgrad_1x1_batched_plan(m: int, nb: int, ci: int, co: int, ncu: int = 256):
-    """(S, mslice, workspace floats) of the batched 1x1 weight gradient: one round of 256x256 tiles over the CUs."""
+def _ctx_wgrad_cus() -> int:
+    """CUs the batched context 1x1 weight gradient is planned for.  It runs on the weight-gradient stream while the
+    critical-path context backward (bilinear-transpose row / cell passes, ctx_bwd_final) runs on the compute stream;
+    a grid of one 512-thread, 256-VGPR block per CU leaves those memory-bound kernels no CU until it drains.
+    224 of 256 measured best (profiles/r2/ab_ctx_wgrad_cus.txt: 441.7-442.4 img/s vs 438.9-440.9 for 256,
+    worse at 192 / 160); CANNET_CTX_WGRAD_CUS overrides."""
+    return int(os.environ.get("CANNET_CTX_WGRAD_CUS", "224"))
+
+
+def wgrad_1x1_batched_plan(m: int, nb: int, ci: int, co: int, ncu: int = 0):
+    """(S, mslice, workspace floats) of the batched 1x1 weight gradient: one round of 256x256 tiles over ncu CUs
+    (0: ``_ctx_wgrad_cus()``)."""
+    ncu = ncu or _ctx_wgrad_cus()
     ntile = (co // 256) * (ci // 256) * nb
     s = max(1, ncu // ntile)
     mslice = -(-m // s)

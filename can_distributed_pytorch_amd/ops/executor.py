@@ -182,7 +182,7 @@ class CANNetExecutor:
         for s in self.back:
             need = max(need, self.ws.plan(n * hh * ww, s.cin, s.cout, 3, False, s.dil)[3])
         need = max(need, self.ws.plan(n * hh * ww, 512, 512, 1, False)[3])
-        need = max(need, C.wgrad_1x1_batched_plan(n * hh * ww, 4, 512, 512)[2])
+        need = max(need, max(C.wgrad_1x1_batched_plan(n * hh * ww, 4, 512, 512, ncu=c)[2] for c in (128, 192, 224, 256)))
         need = max(need, C.conv_wgrad_f1_need(n * h * w))
         self.ws.reserve(need)
         return self.ws
