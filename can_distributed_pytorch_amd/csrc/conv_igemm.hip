@@ -357,6 +357,33 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
   float bs[16];
 #pragma unroll
   for (int c = 0; c < 16; ++c) bs[c] = 0.f;
+  // the epilogue's global reads (ReLU mask / max-pool codes) for ALL pixel fragments, issued before the first
+  // store: the compiler cannot move a load above a store that may alias it, so a per-fragment load was one
+  // exposed memory round trip per fragment (4 * PW per tile).  The main loop's operand registers are dead here.
+  constexpr int NF = 4 * PW;
+  uint4 mk0[EPI == EPI_MASK ? NF : 1], mk1[EPI == EPI_MASK ? NF : 1];
+  uint2 pcw[EPI == EPI_POOLBWD ? NF : 1];
+  if constexpr (EPI == EPI_MASK || EPI == EPI_POOLBWD) {
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      const int m = tile_pix<TP, EPI>(a, pt, wp * 64 * PW + i * 16 + fr);
+      if constexpr (EPI == EPI_MASK) {
+        mk0[i] = make_uint4(0u, 0u, 0u, 0u);
+        mk1[i] = make_uint4(0u, 0u, 0u, 0u);
+        if (m < a.M) {
+          const size_t off = (size_t)m * a.Cout + chb;
+          mk0[i] = *reinterpret_cast<const uint4*>(a.mask + off);
+          mk1[i] = *reinterpret_cast<const uint4*>(a.mask + off + 8);
+        }
+      } else {
+        pcw[i] = make_uint2(0u, 0u);
+        if (m < a.M) pcw[i] = *reinterpret_cast<const uint2*>(a.pcodes + (size_t)m * (a.Cout >> 3) + (chb >> 3));
+      }
+    }
+    // one wait for all of them here: with only stores outstanding afterwards, the per-fragment blocks below need
+    // no vmcnt wait (the compiler otherwise waits for the previous fragment's stores at every block)
+    __builtin_amdgcn_s_waitcnt(0x0F70);             // vmcnt(0), expcnt / lgkmcnt untouched
+  }
 #pragma unroll
   for (int i = 0; i < 4 * PW; ++i) {
     const int m = tile_pix<TP, EPI>(a, pt, wp * 64 * PW + i * 16 + fr);
@@ -376,7 +403,7 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
       const size_t W2 = 2 * (size_t)a.W;
       const size_t b0 = (((size_t)n * 2 * a.H + 2 * ph) * W2 + 2 * pw) * a.Cout + chb;
       const size_t off[4] = {b0, b0 + a.Cout, b0 + W2 * a.Cout, b0 + W2 * a.Cout + a.Cout};
-      const uint2 cw = *reinterpret_cast<const uint2*>(a.pcodes + (size_t)m * (a.Cout >> 3) + (chb >> 3));
+      const uint2 cw = pcw[i];
       float o[4][16];
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
@@ -414,9 +441,8 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
       for (int c = 0; c < 16; c += 4) *reinterpret_cast<float4*>(yf + c) = make_float4(v[c], v[c + 1], v[c + 2], v[c + 3]);
       continue;
     }
-    if (EPI == EPI_MASK) {
-      const uint4 m0 = *reinterpret_cast<const uint4*>(a.mask + off);
-      const uint4 m1 = *reinterpret_cast<const uint4*>(a.mask + off + 8);
+    if constexpr (EPI == EPI_MASK) {
+      const uint4 m0 = mk0[i], m1 = mk1[i];
       const unsigned mw[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
