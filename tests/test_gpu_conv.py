@@ -185,11 +185,15 @@ def test_ring_wgrad_fast_addressing_bitwise(n, h, w, ci, co, dtype, monkeypatch)
     dw0, db0 = torch.empty(co, ci, 3, 3, device="cuda"), torch.empty(co, device="cuda")
     dw1, db1 = torch.empty_like(dw0), torch.empty_like(db0)
     ws = C.WgradWorkspace("cuda")
-    C.conv_wgrad(dy, x, dw0, db0, ksize=3, dil=1, ws=ws)
+    C.conv_wgrad(dy, x, dw0, db0, ksize=3, dil=1, ws=ws)             # FAST + SKEW (default)
+    dw2, db2 = torch.empty_like(dw0), torch.empty_like(db0)
+    monkeypatch.setenv("CANNET_RING_SKEW", "0")                        # FAST, every wave issues DMA
+    C.conv_wgrad(dy, x, dw2, db2, ksize=3, dil=1, ws=ws)
     monkeypatch.setenv("CANNET_RING_FAST", "0")
     C.conv_wgrad(dy, x, dw1, db1, ksize=3, dil=1, ws=ws)
     torch.cuda.synchronize()
     assert torch.equal(dw0, dw1) and torch.equal(db0, db1)
+    assert torch.equal(dw2, dw1) and torch.equal(db2, db1)
     if n * h * w <= 300000:
         wr = torch.zeros(co, ci, 3, 3, device="cuda", requires_grad=True)
         br = torch.zeros(co, device="cuda", requires_grad=True)
