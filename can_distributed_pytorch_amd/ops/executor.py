@@ -92,6 +92,7 @@ class CANNetExecutor:
         self._pack_desc = None          # device descriptor rows of the batched pack launch
         self._pack_desc_ptrs = None
         self.ws = None
+        self.ws_main = None             # conv1_1 weight-gradient slabs when it runs on the compute stream
         self.stream_override = None
         self._side = None
 
@@ -185,7 +186,16 @@ class CANNetExecutor:
         need = max(need, max(C.wgrad_1x1_batched_plan(n * hh * ww, 4, 512, 512, ncu=c)[2] for c in (128, 192, 224, 256)))
         need = max(need, C.conv_wgrad_f1_need(n * h * w))
         self.ws.reserve(need)
+        if self._f0_wgrad_main():
+            if self.ws_main is None:
+                self.ws_main = C.WgradWorkspace(self.head.weight.device)
+            self.ws_main.reserve(self.ws_main.plan(n * h * w, 4, self.front[0].cout, 3, True)[3])
         return self.ws
+
+    @staticmethod
+    def _f0_wgrad_main() -> bool:
+        """CANNET_F0_WGRAD_MAIN=1: conv1_1's weight gradient on the compute stream (see backward_features)."""
+        return os.environ.get("CANNET_F0_WGRAD_MAIN", "0") == "1"
 
     # ----------------------------------------------------------- forward
     def _conv(self, s: ConvSpec, x, epi=C.EPI_BIAS_RELU):
@@ -394,6 +404,19 @@ class CANNetExecutor:
                 self._on_side(side, run_f1, hold, dy2, x)
                 dy, bp = C.conv_f1(dy, dgr, None, x, w1, b1, epi=C.EPI_MASK), None
                 continue
+            if s.idx == 0 and side is not None and self._f0_wgrad_main():
+                # conv1_1's weight gradient on the compute stream, which is otherwise idle once conv1_2's data
+                # gradient is done: it overlaps the tail of conv1_2's (longer) weight gradient on the side stream
+                # instead of queueing behind it.  Own slab workspace: the side stream's is still in use.
+                if self.ws_main is None:
+                    self.ws_main = C.WgradWorkspace(dy.device)
+                C.conv_wgrad(dy, x, grads[s.w_index], grads[s.b_index], ksize=3, dil=1, first=s.first,
+                             ws=self.ws_main, beta=beta, scale=scale, dscale=dscale, bias_partials=bp)
+                # join before marking ready: the bucket holding conv1_1 also holds side-stream gradients, and a
+                # transport that orders its all-reduce after the marking stream must see them too
+                torch.cuda.current_stream(d_b6.device).wait_stream(side)
+                ready([s.w_index, s.b_index])
+                break
             wg(s, dy, x, 3, 1, s.first, s.w_index, s.b_index, bp)
             if s.idx == 0:
                 break

@@ -193,3 +193,24 @@ def test_native_stepper_f1_recompute_matches_stored(monkeypatch):
         assert abs(u - v) <= 1e-3 * abs(u), (la, lb)
     for (name, p0), pa, pb in zip(init, nat_a.parameters(), nat_b.parameters()):
         assert _rel(pb - p0, pa - p0) < 2e-2, name    # the updates, not the weights
+
+
+def test_native_stepper_f0_wgrad_on_compute_stream_bitwise(monkeypatch):
+    """conv1_1's weight gradient on the compute stream (CANNET_F0_WGRAD_MAIN=1, own slab workspace) gives the
+    same weights, bit for bit, as the default schedule on the weight-gradient stream."""
+    from can_distributed_pytorch_amd.engine.native import NativeStepper
+    _, nat_a = _models(8)
+    nat_b = copy.deepcopy(nat_a)
+    x = torch.randn(2, 3, 96, 128, device="cuda")
+    gt = torch.rand(2, 1, 12, 16, device="cuda")
+    a = NativeStepper("cuda", lr=1e-4, graph=False, model=nat_a)
+    b = NativeStepper("cuda", lr=1e-4, graph=False, model=nat_b)
+    for _ in range(3):
+        monkeypatch.setenv("CANNET_F0_WGRAD_MAIN", "0")
+        a.step(x, gt)
+        monkeypatch.setenv("CANNET_F0_WGRAD_MAIN", "1")
+        b.step(x, gt)
+    torch.cuda.synchronize()
+    assert b.ex.ws_main is not None
+    for (name, pa), pb in zip(nat_a.named_parameters(), nat_b.parameters()):
+        assert torch.equal(pa, pb), name
