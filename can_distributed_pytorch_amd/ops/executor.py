@@ -447,7 +447,8 @@ class CANNetExecutor:
             return None
         dev = self.head.weight.device
         if self._side is None or self._side.device != dev:
-            self._side = torch.cuda.Stream(dev)
+            # CANNET_SIDE_PRIORITY=-1: high-priority weight-gradient stream (its work ends the step)
+            self._side = torch.cuda.Stream(dev, priority=int(os.environ.get("CANNET_SIDE_PRIORITY", "0")))
         return self._side
 
     @staticmethod
