@@ -39,6 +39,12 @@ int can_conv_wgrad_f1(const void* dy, const void* img, const void* w1, const flo
                       float* dw, float* db, int N, int H, int W, int S, float beta, float scale, const float* dscale,
                       int dt, void* stream);
 
+// conv1_2's data gradient with conv1_1's weight gradient fused (slabs [S][36][64] + [S][64]; returns S or < 0)
+int can_conv_ws64_dgrad_w1g(const void* dy, const void* w, const void* mask, const void* img, void* y, float* w1slab,
+                            float* w1bslab, int slab_cap, int N, int H, int W, int dt, void* stream);
+int can_wgrad_reduce_first(const float* ws, const float* wsb, float* dw, float* db, int S, float beta, float scale,
+                           const float* dscale, void* stream);
+
 // elementwise.hip
 int can_maxpool_fwd(const void* x, void* y, void* codes, int N, int H, int W, int C, int dt, void* stream);
 int can_maxpool_bwd_codes(const void* codes, const void* dy, void* dx, int N, int H, int W, int C, int dt,

@@ -107,6 +107,20 @@ PYBIND11_MODULE(CAN_MODULE_NAME, m) {
                       P(stream)),
           "conv_f1");
   });
+  m.def("conv_ws64_dgrad_w1g", [](uintptr_t dy, uintptr_t w, uintptr_t mask, uintptr_t img, uintptr_t y,
+                                  uintptr_t w1slab, uintptr_t w1bslab, int slab_cap, int N, int H, int W, int dt,
+                                  uintptr_t stream) {
+    const int S = can_conv_ws64_dgrad_w1g(P(dy), P(w), P(mask), P(img), P(y), (float*)w1slab, (float*)w1bslab,
+                                          slab_cap, N, H, W, dt, P(stream));
+    if (S <= 0) check(S == 0 ? -1 : S, "conv_ws64_dgrad_w1g");
+    return S;
+  });
+  m.def("wgrad_reduce_first", [](uintptr_t ws, uintptr_t wsb, uintptr_t dw, uintptr_t db, int S, float beta,
+                                 float scale, uintptr_t dscale, uintptr_t stream) {
+    check(can_wgrad_reduce_first((const float*)ws, (const float*)wsb, (float*)dw, (float*)db, S, beta, scale,
+                                 (const float*)dscale, P(stream)),
+          "wgrad_reduce_first");
+  });
   m.def("conv_wgrad_f1", [](uintptr_t dy, uintptr_t img, uintptr_t w1, uintptr_t b1, uintptr_t ws, uintptr_t wsb,
                             uintptr_t dw, uintptr_t db, int N, int H, int W, int S, float beta, float scale,
                             uintptr_t dscale, int dt, uintptr_t stream) {

@@ -882,6 +882,11 @@ struct HaloConvArgs {
   uint32_t* codes = nullptr;
   // EPI_MASK (not F1): bias-gradient partials of the produced dY, [ntile * rows per tile][CO] fp32
   float* bpart = nullptr;
+  // conv_ws64_kernel<.., EPI_MASK, W1G>: conv1_1's weight gradient from the dY tile it just produced (img =
+  // the NHWC4 network input): per-block partial slabs w1slab [2 * grid][36][64] (k = tap*4 + c) and
+  // w1bslab [2 * grid][64] (bias), reduced by the first-layer slab reduction; y may be null (dY not stored)
+  float* w1slab = nullptr;
+  float* w1bslab = nullptr;
 };
 
 template <int DT, int CO, int EPI, int TCOL, int F1 = 0>
@@ -1188,7 +1193,7 @@ conv_halo64_kernel(HaloConvArgs a) {
 // earlier (a counted wait would be unsafe: loads and stores retire out of
 // order with respect to each other).
 // ===========================================================================
-template <int DT, int EPI>
+template <int DT, int EPI, bool W1G = false>
 __global__ void __launch_bounds__(512, 1) conv_ws64_kernel(HaloConvArgs a) {
   // halo rows of 66 pixels stored at a 72-pixel stride: a 1-KiB DMA piece (8 pixels) never straddles two
   // rows, so wave w fetches piece column w of all 6 rows (pixel slot 8w + lane / 8, a per-lane constant)
@@ -1199,6 +1204,13 @@ __global__ void __launch_bounds__(512, 1) conv_ws64_kernel(HaloConvArgs a) {
   constexpr int HALO_BYTES = NHI * 1024;
   static_assert(EPI == EPI_BIAS_RELU || EPI == EPI_BIAS || EPI == EPI_NONE || EPI == EPI_MASK ||
                 EPI == EPI_POOLFWD, "ws64 epilogues");
+  static_assert(!W1G || EPI == EPI_MASK, "W1G: conv1_2 data gradient only");
+  // W1G: image halo of the tile in LDS after the two halo buffers, one planar copy per (kw, c) shifted by kw so a
+  // B fragment (8 consecutive pixels of one tap / channel) is one aligned 16-B read: [3][4][6 rows][72] 16-bit
+  constexpr int IMG_RS = 72, IMG_PLANE = (TR + 2) * IMG_RS;
+  // then the raw image halo (6 x 66 pixels x 8 B, LDS-DMA'd at the tile start: 13 waves x 64 dwords) and the
+  // wave-private fp32 weight-gradient accumulators (8 waves x 3 x 64 lanes x 16 B; registers only in that phase)
+  constexpr int IMG_PLANES_BYTES = 12 * IMG_PLANE * 2, IMG_RAW_BYTES = 13 * 256;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1273,7 +1285,18 @@ __global__ void __launch_bounds__(512, 1) conv_ws64_kernel(HaloConvArgs a) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
       hoff[kw][kk] = (r * HCP + fr + kw) * 128 + (((kk * 4 + fq) ^ ((fr + kw) & 7)) * 16);
+  if constexpr (W1G) {
+    f32x4* z = reinterpret_cast<f32x4*>(smem + 2 * HALO_BYTES + IMG_PLANES_BYTES + IMG_RAW_BYTES) + wave * 192 + lane;
+#pragma unroll
+    for (int nb = 0; nb < 3; ++nb) z[nb * 64] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  // W1G: conv1_1 weight-gradient accumulators of this wave (16 output channels cb*16.., the 3 x 16 k columns
+  // n = tap*4 + c (n = 36: the bias, through a column of ones), pixel rows 2*ph, 2*ph + 1 of every tile), kept in
+  // LDS between tiles (the main loop is at the VGPR cap)
+  unsigned short* imgs = reinterpret_cast<unsigned short*>(smem + 2 * HALO_BYTES);
+  unsigned char* imgraw = smem + 2 * HALO_BYTES + IMG_PLANES_BYTES;
+  f32x4* waccl = reinterpret_cast<f32x4*>(smem + 2 * HALO_BYTES + IMG_PLANES_BYTES + IMG_RAW_BYTES) + wave * 192 + lane;
 
   for (int t = t0, it = 0; t < t1; ++t, ++it) {
     unsigned char* cur = smem + (it & 1) * HALO_BYTES;
@@ -1282,6 +1305,27 @@ __global__ void __launch_bounds__(512, 1) conv_ws64_kernel(HaloConvArgs a) {
     tile_org(t, n, oh0, ow0);
     const int oh = oh0 + r;
     const bool row_ok = oh < a.H;
+    if constexpr (W1G) {
+      // raw image halo of this tile -> imgraw by LDS-DMA (4 B per lane; dword d = pixel * 2 + half), retired by
+      // the wait after the main loop
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int wj = j * 8 + wave;                 // wave-uniform
+        if (wj < 13) {
+          int ln = lane;
+          asm volatile("" : "+v"(ln));
+          const int d = wj * 64 + ln, px = d >> 1;
+          const int hr = px / 66, hc = px - hr * 66;
+          const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
+          const bool ok = hr < 6 && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+          const void* src = ok ? (const void*)(reinterpret_cast<const unsigned char*>(a.img) +
+                                               ((size_t)(n * a.H + ih) * a.W + iw) * 8 + (d & 1) * 4)
+                               : (const void*)a.zero;
+          __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(imgraw + wj * 256), 4, 0,
+                                           0);
+        }
+      }
+    }
     uint4 mk[4];
     if constexpr (EPI == EPI_MASK) {
 #pragma unroll
@@ -1335,9 +1379,9 @@ __global__ void __launch_bounds__(512, 1) conv_ws64_kernel(HaloConvArgs a) {
           v[c] = pos_bits((unsigned short)(mw[c >> 1] >> ((c & 1) * 16))) ? v[c] : 0.f;
       }
       const uint4 o = pack8h<DT>(v);
-      if (row_ok && ow < a.W && (EPI != EPI_POOLFWD || a.y != nullptr))
+      if (row_ok && ow < a.W && ((EPI != EPI_POOLFWD && !W1G) || a.y != nullptr))
         *reinterpret_cast<uint4*>(a.y + ((size_t)(n * a.H + oh) * a.W + ow) * 64 + chb) = o;
-      if constexpr (EPI == EPI_POOLFWD) {
+      if constexpr (EPI == EPI_POOLFWD || W1G) {
         // staging tile [4 rows][64 cols] x 128 B in `cur`, 16-B chunk c of column col at slot c ^ (col & 7)
         reinterpret_cast<uint4*>(cur + (r * 64 + col) * 128)[(h * 4 + fq) ^ (col & 7)] = o;
       }
@@ -1369,13 +1413,94 @@ __global__ void __launch_bounds__(512, 1) conv_ws64_kernel(HaloConvArgs a) {
       // staging reads done before the next-but-one halo DMA overwrites `cur`
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
+    if constexpr (W1G) {
+      // image halo -> 12 shifted planes: imgs[(kw*4 + c)*IMG_PLANE + hr*IMG_RS + j] = img[hr][j + kw][c]
+      // (imgraw retired by the wait + barrier after the main loop; the planes' previous readers passed the
+      // barrier that ended the previous tile)
+      if (tid < 6 * 66) {
+        int tl = tid;
+        asm volatile("" : "+v"(tl));
+        const int hr = tl / 66, hc = tl - hr * 66;
+        const uint2 imv = *reinterpret_cast<const uint2*>(imgraw + tl * 8);
+        const unsigned short cv[4] = {(unsigned short)(imv.x & 0xffffu), (unsigned short)(imv.x >> 16),
+                                      (unsigned short)(imv.y & 0xffffu), (unsigned short)(imv.y >> 16)};
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw)
+          if (hc - kw >= 0 && hc - kw < IMG_RS)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) imgs[(kw * 4 + c) * IMG_PLANE + hr * IMG_RS + hc - kw] = cv[c];
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // dY staging tile + image planes
+      // dW1[co][n] += sum_p dY[p][co] * img(p + tap)[c], K = this wave's 128 pixels in 4 steps of 32
+      const int cb = wave & 3, ph = wave >> 2;
+      int ln = lane;
+      asm volatile("" : "+v"(ln));                   // lane math stays in this phase (not hoisted out of the loop)
+      const int fr = ln & 15, fq = ln >> 4;
+      const int co = cb * 16 + fr;
+      f32x4 wacc[3];
+#pragma unroll
+      for (int nb = 0; nb < 3; ++nb) wacc[nb] = waccl[nb * 64];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const int row = 2 * ph + (s4 >> 1), colb = (s4 & 1) * 32 + fq * 8;
+        unsigned av[4];
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+          const int c0 = colb + e, c1 = colb + e + 1;
+          const unsigned short u0 = *reinterpret_cast<const unsigned short*>(
+              cur + (row * 64 + c0) * 128 + (((co >> 3) ^ (c0 & 7)) * 16) + (co & 7) * 2);
+          const unsigned short u1 = *reinterpret_cast<const unsigned short*>(
+              cur + (row * 64 + c1) * 128 + (((co >> 3) ^ (c1 & 7)) * 16) + (co & 7) * 2);
+          av[e >> 1] = (unsigned)u0 | ((unsigned)u1 << 16);
+        }
+        const frag8_t afr = __builtin_bit_cast(frag8_t, make_uint4(av[0], av[1], av[2], av[3]));
+#pragma unroll
+        for (int nb = 0; nb < 3; ++nb) {
+          const int nn = nb * 16 + fr;
+          const int tap = (nn < 36) ? (nn >> 2) : 0, c = nn & 3;
+          const int kh = tap / 3, kw = tap - kh * 3;
+          uint4 bv = *reinterpret_cast<const uint4*>(imgs + (kw * 4 + c) * IMG_PLANE + (row + kh) * IMG_RS + colb);
+          if (nn >= 36) {
+            const unsigned one2 = (nn == 36) ? ((unsigned)one_bits<DT>() * 0x10001u) : 0u;
+            bv = make_uint4(one2, one2, one2, one2);
+          }
+          wacc[nb] = mfma16<DT>(afr, __builtin_bit_cast(frag8_t, bv), wacc[nb]);
+        }
+      }
+#pragma unroll
+      for (int nb = 0; nb < 3; ++nb) waccl[nb * 64] = wacc[nb];
+      // staging / image reads done before the next tile's epilogue and the next-but-one halo DMA overwrite them
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+  }
+  if constexpr (W1G) {
+    // D row fq*4 + q = channel cb*16 + fq*4 + q, column fr = k column nb*16 + fr; part = 2 * block + ph
+    const int cb = wave & 3, ph = wave >> 2;
+    const size_t part = (size_t)blockIdx.x * 2 + ph;
+#pragma unroll
+    for (int nb = 0; nb < 3; ++nb) {
+      const int nn = nb * 16 + fr;
+      const f32x4 w4 = waccl[nb * 64];
+      const float4 v4 = make_float4(w4[0], w4[1], w4[2], w4[3]);
+      if (nn < 36)
+        *reinterpret_cast<float4*>(a.w1slab + (part * 36 + nn) * 64 + cb * 16 + fq * 4) = v4;
+      else if (nn == 36)
+        *reinterpret_cast<float4*>(a.w1bslab + part * 64 + cb * 16 + fq * 4) = v4;
+    }
   }
 }
 
-template <int DT, int EPI>
+// grid of launch_ws64 for ntile tiles (W1G: 2 weight-gradient slabs per block)
+static int ws64_grid(int ntile, int ncu) {
+  const int per = (ntile + ncu - 1) / ncu;
+  return (ntile + per - 1) / per;
+}
+
+template <int DT, int EPI, bool W1G = false>
 static int launch_ws64(const HaloConvArgs& a, hipStream_t s) {
-  constexpr size_t lds = 2 * (size_t)(6 * 9) * 1024;       // 2 halo buffers of 6 rows x 72 pixel slots
-  auto kfn = conv_ws64_kernel<DT, EPI>;
+  // 2 halo buffers of 6 rows x 72 pixel slots (+ W1G: 12 shifted image planes of 6 x 72 16-bit words)
+  constexpr size_t lds = 2 * (size_t)(6 * 9) * 1024 + (W1G ? 12 * 6 * 72 * 2 + 13 * 256 + 8 * 192 * 16 : 0);
+  auto kfn = conv_ws64_kernel<DT, EPI, W1G>;
   static int ncu = 0;
   if (!ncu) {
     CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -1383,9 +1508,7 @@ static int launch_ws64(const HaloConvArgs& a, hipStream_t s) {
     CAN_HIP_CHECK(hipGetDevice(&dev));
     CAN_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
   }
-  const int ntile = a.N * a.tiles_y * a.tiles_x;
-  const int per = (ntile + ncu - 1) / ncu;
-  const int grid = (ntile + per - 1) / per;       // every block gets a non-empty run
+  const int grid = ws64_grid(a.N * a.tiles_y * a.tiles_x, ncu);   // every block gets a non-empty run
   hipLaunchKernelGGL(kfn, dim3(grid), dim3(512), lds, s, a);
   return (int)hipGetLastError();
 }
@@ -1736,7 +1859,35 @@ static int conv_f1_impl(const void* x, const void* w, const float* bias, const v
   return -6;
 }
 
+// conv1_2's data gradient (ws64, EPI_MASK: dX = relu-masked, mask = conv1_1's output) with conv1_1's weight
+// gradient accumulated from each produced tile (W1G); dX stored only when y is not null.  Writes 2 * grid slabs to
+// w1slab [S][36][64] / w1bslab [S][64]; returns S (> 0) or a negative error.
+template <int DT>
+static int conv_ws64_dgrad_w1g_impl(const void* dy, const void* w, const void* mask, const void* img, void* y,
+                                    float* w1slab, float* w1bslab, int slab_cap, int N, int H, int W, hipStream_t s) {
+  HaloConvArgs h;
+  h.x = (const bf16_t*)dy; h.w = (const bf16_t*)w; h.bias = nullptr; h.mask = (const bf16_t*)mask;
+  h.y = (bf16_t*)y; h.zero = conv_zero_page();
+  if (!h.zero) return -10;
+  h.img = (const bf16_t*)img; h.w1slab = w1slab; h.w1bslab = w1bslab;
+  h.N = N; h.H = H; h.W = W; h.tiles_x = (W + 63) / 64; h.tiles_y = (H + 3) / 4;
+  int dev = 0, ncu = 0;
+  CAN_HIP_CHECK(hipGetDevice(&dev));
+  CAN_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  const int S = 2 * ws64_grid(N * h.tiles_y * h.tiles_x, ncu);
+  if (S > slab_cap) return -12;
+  const int rc = launch_ws64<DT, EPI_MASK, true>(h, s);
+  return rc ? -rc : S;
+}
+
 }  // namespace can
+
+extern "C" int can_conv_ws64_dgrad_w1g(const void* dy, const void* w, const void* mask, const void* img, void* y,
+                                       float* w1slab, float* w1bslab, int slab_cap, int N, int H, int W, int dt,
+                                       void* stream) {
+  CAN_DT_DISPATCH(dt, can::conv_ws64_dgrad_w1g_impl<DT>(dy, w, mask, img, y, w1slab, w1bslab, slab_cap, N, H, W,
+                                                        (hipStream_t)stream));
+}
 
 extern "C" int can_conv_f1(const void* x, const void* w, const float* bias, const void* img, const void* w1,
                            const float* b1, void* y, int N, int H, int W, int epi, int dt, void* stream) {

@@ -1596,6 +1596,12 @@ static int conv_wgrad_f1_impl(const void* dy, const void* img, const void* w1, c
   return launch_reduce2(ws, h.wsb, dw, db, S, S, 576, 64, 64, 9, 0, beta, scale, dscale, s);
 }
 
+// first-layer slab reduction: ws [S][36][64] (k = tap*4 + c), wsb [S][64] -> dW [64][3][3][3], db [64]
+extern "C" int can_wgrad_reduce_first(const float* ws, const float* wsb, float* dw, float* db, int S, float beta,
+                                      float scale, const float* dscale, void* stream) {
+  return launch_reduce2(ws, wsb, dw, db, S, S, 36, 64, 4, 9, 1, beta, scale, dscale, (hipStream_t)stream);
+}
+
 extern "C" int can_conv_wgrad_f1(const void* dy, const void* img, const void* w1, const float* b1, float* ws,
                                  float* wsb, float* dw, float* db, int N, int H, int W, int S, float beta, float scale,
                                  const float* dscale, int dt, void* stream) {

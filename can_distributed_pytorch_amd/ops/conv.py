@@ -489,3 +489,47 @@ def conv_wgrad_f1(dy: torch.Tensor, img: torch.Tensor, w1pack: torch.Tensor, b1:
                     buf.data_ptr() + 4 * s * 576 * 64, dw.data_ptr(), db.data_ptr() if db is not None else 0, n, h, w,
                     s, float(beta), float(scale), dscale.data_ptr() if dscale is not None else 0, dt_code(dt),
                     _ext.stream_ptr(img.device))
+
+
+def w1g_slab_cap(device) -> int:
+    """Slab rows conv_dgrad_w1g may write: 2 per block of the one-block-per-CU ws64 grid."""
+    return 2 * torch.cuda.get_device_properties(device).multi_processor_count
+
+
+def conv_dgrad_w1g(dy: torch.Tensor, wpack: torch.Tensor, mask: torch.Tensor, img: torch.Tensor, dw1: torch.Tensor,
+                   db1: torch.Tensor, *, slabs: torch.Tensor, bslabs: torch.Tensor, store_dx: bool = False,
+                   beta: float = 0.0, scale: float = 1.0, dscale: Optional[torch.Tensor] = None):
+    """conv1_2's data gradient with conv1_1's weight gradient fused into it (weight-stationary ws64 kernel).
+
+    dX = conv(dy, flipped conv1_2 wpack) * (mask > 0) with mask = conv1_1's output; every produced 4 x 64 tile
+    is multiplied on the MFMA with the matching image patches (img = NHWC4 network input) into per-block fp32
+    partials, so conv1_1's weight gradient never re-reads dX from memory; one deterministic slab reduction
+    writes dw1 [64,3,3,3] / db1 [64] (beta / scale / dscale as conv_wgrad).  dX (conv1_1's dY, never needed
+    again) is returned only with store_dx.  slabs / bslabs: fp32 [w1g_slab_cap, 36*64] / [w1g_slab_cap, 64].
+    """
+    C = _ext.require()
+    dt = dy.dtype
+    n, h, w, c = dy.shape
+    if c != 64 or tuple(mask.shape) != (n, h, w, 64) or tuple(img.shape) != (n, h, w, 4):
+        raise ValueError(f"conv_dgrad_w1g: dy/mask [N,H,W,64], img [N,H,W,4]; got {tuple(dy.shape)}, "
+                         f"{tuple(mask.shape)}, {tuple(img.shape)}")
+    for t, nm in ((dy, "dy"), (mask, "mask"), (img, "img")):
+        _check_act(t, nm, dtype=dt)
+    if tuple(wpack.shape) != (64, 576) or wpack.dtype != dt or not wpack.is_contiguous():
+        raise ValueError("wpack must be the packed [64, 9*64] conv1_2 data-gradient weight")
+    if tuple(dw1.shape) != (64, 3, 3, 3) or tuple(db1.shape) != (64,):
+        raise ValueError("dw1 / db1 must be conv1_1's [64,3,3,3] / [64] gradients")
+    for t, nm in ((dw1, "dw1"), (db1, "db1"), (slabs, "slabs"), (bslabs, "bslabs")):
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.device != dy.device:
+            raise ValueError(f"{nm} must be a contiguous fp32 tensor on {dy.device}")
+    cap = slabs.shape[0]
+    if slabs.dim() != 2 or slabs.shape[1] != 36 * 64 or tuple(bslabs.shape) != (cap, 64):
+        raise ValueError("slabs / bslabs must be [cap, 36*64] / [cap, 64]")
+    out = torch.empty_like(dy) if store_dx else None
+    st = _ext.stream_ptr(dy.device)
+    s = C.conv_ws64_dgrad_w1g(dy.data_ptr(), wpack.data_ptr(), mask.data_ptr(), img.data_ptr(),
+                              out.data_ptr() if out is not None else 0, slabs.data_ptr(), bslabs.data_ptr(), cap,
+                              n, h, w, dt_code(dt), st)
+    C.wgrad_reduce_first(slabs.data_ptr(), bslabs.data_ptr(), dw1.data_ptr(), db1.data_ptr(), s, float(beta),
+                         float(scale), dscale.data_ptr() if dscale is not None else 0, st)
+    return out

@@ -93,6 +93,7 @@ class CANNetExecutor:
         self._pack_desc_ptrs = None
         self.ws = None
         self.ws_main = None             # conv1_1 weight-gradient slabs when it runs on the compute stream
+        self._w1g_buf = None            # conv1_1 weight-gradient slabs of the fused conv1_2 data gradient
         self.stream_override = None
         self._side = None
 
@@ -186,11 +187,26 @@ class CANNetExecutor:
         need = max(need, max(C.wgrad_1x1_batched_plan(n * hh * ww, 4, 512, 512, ncu=c)[2] for c in (128, 192, 224, 256)))
         need = max(need, C.conv_wgrad_f1_need(n * h * w))
         self.ws.reserve(need)
+        if os.environ.get("CANNET_W1G", "0") == "1":
+            self._w1g_slabs(self.head.weight.device)
         if self._f0_wgrad_main():
             if self.ws_main is None:
                 self.ws_main = C.WgradWorkspace(self.head.weight.device)
             self.ws_main.reserve(self.ws_main.plan(n * h * w, 4, self.front[0].cout, 3, True)[3])
         return self.ws
+
+    def _w1g_ok(self, x) -> bool:
+        """CANNET_W1G=1: conv1_1's weight gradient fused into conv1_2's data gradient (conv_dgrad_w1g)."""
+        f0, f1 = self.front[0], self.front[1]
+        return (os.environ.get("CANNET_W1G", "0") == "1" and f0.first and f0.cout == 64 and f1.cin == 64
+                and f1.cout == 64 and not f0.pool_after and x.dim() == 4 and x.shape[-1] == 64)
+
+    def _w1g_slabs(self, device):
+        if self._w1g_buf is None or self._w1g_buf[0].device != device:
+            cap = C.w1g_slab_cap(device)
+            self._w1g_buf = (torch.empty(cap, 36 * 64, dtype=torch.float32, device=device),
+                             torch.empty(cap, 64, dtype=torch.float32, device=device))
+        return self._w1g_buf
 
     @staticmethod
     def _f0_wgrad_main() -> bool:
@@ -422,6 +438,18 @@ class CANNetExecutor:
                 break
             _, dgr = self.packs[id(s.module.weight)]
             prev = self.front[s.idx - 1]
+            if s.idx == 1 and prev.first and self._w1g_ok(x):
+                # conv1_2's data gradient with conv1_1's weight gradient fused (compute stream): conv1_1's dY is
+                # consumed tile by tile inside the kernel, never written to or re-read from memory
+                img = sv["front_in"][0]
+                sl, bsl = self._w1g_slabs(x.device)
+                C.conv_dgrad_w1g(dy, dgr, x, img, grads[prev.w_index], grads[prev.b_index], slabs=sl, bslabs=bsl,
+                                 beta=beta, scale=scale, dscale=dscale)
+                if side is not None:
+                    # the bucket holding conv1_1 also holds side-stream gradients (see the F0 path above)
+                    torch.cuda.current_stream(d_b6.device).wait_stream(side)
+                ready([prev.w_index, prev.b_index])
+                break
             if prev.pool_after:
                 # data gradient at the pooled resolution, scattered through the max-pool backward
                 # (+ ReLU mask of the pool input) in the conv epilogue: the pooled gradient never

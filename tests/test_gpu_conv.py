@@ -459,3 +459,40 @@ def test_conv_igemm_batched_matches_per_item(n, h, w, ci, co, k, epi):
     ref = torch.stack([C.conv_igemm(x[i], wp[i], None, ksize=k, epi=epi) for i in range(nb)])
     torch.cuda.synchronize()
     assert torch.equal(y, ref)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("n,h,w,beta", [(2, 40, 128, 0.0), (1, 37, 150, 0.0), (2, 13, 70, 1.0), (1, 256, 512, 0.0)])
+def test_conv_dgrad_w1g_fused(n, h, w, beta, dtype):
+    """conv1_2's data gradient with conv1_1's weight gradient fused (ws64 W1G): dX bitwise equal to the plain ws64
+    data gradient; dW1 / db1 vs fp32 PyTorch of conv1_1's weight gradient from that dX (ragged tiles, beta)."""
+    from can_distributed_pytorch_amd.ops import conv as C
+    torch.manual_seed(11)
+    dev = "cuda"
+    wt = (torch.randn(64, 64, 3, 3, device=dev) * 0.05).to(dtype).float()
+    dgr = C.pack_weight_dgrad(wt, dtype)
+    dy = torch.randn(n, h, w, 64, device=dev).to(dtype)
+    mask = torch.randn(n, h, w, 64, device=dev).to(dtype)
+    img = torch.randn(n, 3, h, w, device=dev)
+    x4 = C.to_nhwc4(img, dtype)
+    dx_ref = C.conv_igemm(dy, dgr, None, ksize=3, epi=C.EPI_MASK, mask=mask)
+    cap = C.w1g_slab_cap(dev)
+    sl = torch.full((cap, 36 * 64), float("nan"), device=dev)
+    bsl = torch.full((cap, 64), float("nan"), device=dev)
+    dw0 = torch.randn(64, 3, 3, 3, device=dev)
+    db0 = torch.randn(64, device=dev)
+    dw, db = dw0.clone(), db0.clone()
+    dx = C.conv_dgrad_w1g(dy, dgr, mask, x4, dw, db, slabs=sl, bslabs=bsl, store_dx=True, beta=beta)
+    torch.cuda.synchronize()
+    assert torch.equal(dx, dx_ref)
+    wr = torch.zeros(64, 3, 3, 3, device=dev, requires_grad=True)
+    br = torch.zeros(64, device=dev, requires_grad=True)
+    y = F.conv2d(x4[..., :3].float().permute(0, 3, 1, 2), wr, br, padding=1)
+    gw, gb = torch.autograd.grad(y, (wr, br), dx_ref.float().permute(0, 3, 1, 2))
+    _close(dw, gw + beta * dw0, 1e-2)
+    _close(db, gb + beta * db0, 1e-2)
+    # against the unfused first-layer weight gradient of the same dX
+    dw2, db2 = dw0.clone(), db0.clone()
+    C.conv_wgrad(dx_ref, x4, dw2, db2, ksize=3, first=True, beta=beta)
+    _close(dw, dw2, 5e-3)
+    _close(db, db2, 5e-3)

@@ -214,3 +214,29 @@ def test_native_stepper_f0_wgrad_on_compute_stream_bitwise(monkeypatch):
     assert b.ex.ws_main is not None
     for (name, pa), pb in zip(nat_a.named_parameters(), nat_b.parameters()):
         assert torch.equal(pa, pb), name
+
+
+def test_native_stepper_w1g_fused_matches_default(monkeypatch):
+    """conv1_1's weight gradient fused into conv1_2's data gradient (CANNET_W1G=1) trains like the default
+    schedule (same kernels elsewhere; the fused product sums in a different order)."""
+    from can_distributed_pytorch_amd.engine.native import NativeStepper
+    _, nat_a = _models(9)
+    nat_b = copy.deepcopy(nat_a)
+    init = [(n, p.detach().clone()) for n, p in nat_a.named_parameters()]
+    x = torch.randn(2, 3, 96, 128, device="cuda")
+    gt = torch.rand(2, 1, 12, 16, device="cuda")
+    a = NativeStepper("cuda", lr=1e-7, graph=False, model=nat_a)
+    b = NativeStepper("cuda", lr=1e-7, graph=False, model=nat_b)
+    la, lb = [], []
+    for _ in range(3):
+        monkeypatch.setenv("CANNET_W1G", "0")
+        la.append(float(a.step(x, gt)))
+        monkeypatch.setenv("CANNET_W1G", "1")
+        lb.append(float(b.step(x, gt)))
+    torch.cuda.synchronize()
+    assert b.ex._w1g_buf is not None
+    assert la[0] == lb[0]
+    for u, v in zip(la, lb):
+        assert abs(u - v) <= 1e-3 * abs(u), (la, lb)
+    for (name, p0), pa, pb in zip(init, nat_a.parameters(), nat_b.parameters()):
+        assert _rel(pb - p0, pa - p0) < 1e-2, name
