@@ -187,7 +187,7 @@ class CANNetExecutor:
         need = max(need, max(C.wgrad_1x1_batched_plan(n * hh * ww, 4, 512, 512, ncu=c)[2] for c in (128, 192, 224, 256)))
         need = max(need, C.conv_wgrad_f1_need(n * h * w))
         self.ws.reserve(need)
-        if os.environ.get("CANNET_W1G", "0") == "1":
+        if os.environ.get("CANNET_W1G", "1") != "0":
             self._w1g_slabs(self.head.weight.device)
         if self._f0_wgrad_main():
             if self.ws_main is None:
@@ -196,9 +196,11 @@ class CANNetExecutor:
         return self.ws
 
     def _w1g_ok(self, x) -> bool:
-        """CANNET_W1G=1: conv1_1's weight gradient fused into conv1_2's data gradient (conv_dgrad_w1g)."""
+        """conv1_1's weight gradient fused into conv1_2's data gradient (conv_dgrad_w1g; CANNET_W1G=0: separate
+        weight-gradient launch on the side stream).  Measured 453.5 -> 456.7 img/s, peak HBM 8.75 -> 7.95 GB
+        (profiles/r2/ab_w1g.txt)."""
         f0, f1 = self.front[0], self.front[1]
-        return (os.environ.get("CANNET_W1G", "0") == "1" and f0.first and f0.cout == 64 and f1.cin == 64
+        return (os.environ.get("CANNET_W1G", "1") != "0" and f0.first and f0.cout == 64 and f1.cin == 64
                 and f1.cout == 64 and not f0.pool_after and x.dim() == 4 and x.shape[-1] == 64)
 
     def _w1g_slabs(self, device):

@@ -203,6 +203,7 @@ def test_native_stepper_f0_wgrad_on_compute_stream_bitwise(monkeypatch):
     nat_b = copy.deepcopy(nat_a)
     x = torch.randn(2, 3, 96, 128, device="cuda")
     gt = torch.rand(2, 1, 12, 16, device="cuda")
+    monkeypatch.setenv("CANNET_W1G", "0")                # conv1_1's separate weight-gradient launch
     a = NativeStepper("cuda", lr=1e-4, graph=False, model=nat_a)
     b = NativeStepper("cuda", lr=1e-4, graph=False, model=nat_b)
     for _ in range(3):
@@ -217,7 +218,7 @@ def test_native_stepper_f0_wgrad_on_compute_stream_bitwise(monkeypatch):
 
 
 def test_native_stepper_w1g_fused_matches_default(monkeypatch):
-    """conv1_1's weight gradient fused into conv1_2's data gradient (CANNET_W1G=1) trains like the default
+    """conv1_1's weight gradient fused into conv1_2's data gradient (CANNET_W1G=1, the default) trains like the separate-launch
     schedule (same kernels elsewhere; the fused product sums in a different order)."""
     from can_distributed_pytorch_amd.engine.native import NativeStepper
     _, nat_a = _models(9)
