@@ -39,6 +39,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace py = pybind11;
@@ -73,35 +74,65 @@ static ncclRedOp_t to_op(int code) {
   throw std::runtime_error("unsupported reduce op");
 }
 
+// The communicator is created NON-blocking (ncclConfig_t.blocking = 0) so that its
+// initialisation is bounded: a rank whose peers never join (one rank failed
+// before or inside its own init) polls ncclCommGetAsyncError until init_timeout_s,
+// then aborts the half-made communicator and throws — every rank gets back to
+// Python, where parallel/reducer.py agrees over the torch process group on
+// falling back together.  In non-blocking mode any RCCL call may return
+// ncclInProgress (e.g. the first collective's lazy connection setup): call()
+// polls the communicator until that completes (bounded too) before the next call.
 class RcclComm {
  public:
-  RcclComm(int rank, int world, const std::string& uid, int device) : rank_(rank), world_(world), device_(device) {
+  RcclComm(int rank, int world, const std::string& uid, int device, double init_timeout_s)
+      : rank_(rank), world_(world), device_(device), timeout_(init_timeout_s) {
     if (uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("bad ncclUniqueId size");
     ncclUniqueId id;
     memcpy(&id, uid.data(), sizeof(id));
     hip_check(hipSetDevice(device), "hipSetDevice");
-    nccl_check(ncclCommInitRank(&comm_, world, id, rank), "ncclCommInitRank");
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclResult_t r = ncclCommInitRankConfig(&comm_, world, id, rank, &cfg);
+    if (r != ncclSuccess && r != ncclInProgress) {
+      if (comm_) ncclCommAbort(comm_);
+      comm_ = nullptr;
+      nccl_check(r, "ncclCommInitRankConfig");
+    }
+    try {
+      settle("ncclCommInitRankConfig");
+    } catch (...) {
+      if (comm_) ncclCommAbort(comm_);
+      comm_ = nullptr;
+      throw;
+    }
   }
   ~RcclComm() {
     if (comm_) ncclCommDestroy(comm_);
   }
+  // Every RCCL call on this communicator goes through here: ncclInProgress is settled, anything else thrown.
+  void call(ncclResult_t r, const char* what) {
+    if (r == ncclInProgress) {
+      settle(what);
+      return;
+    }
+    nccl_check(r, what);
+  }
   void allreduce(uintptr_t ptr, size_t count, int dtype, int op, uintptr_t stream) {
-    nccl_check(ncclAllReduce((const void*)ptr, (void*)ptr, count, to_dtype(dtype), to_op(op), comm_,
-                             (hipStream_t)stream),
-               "ncclAllReduce");
+    call(ncclAllReduce((const void*)ptr, (void*)ptr, count, to_dtype(dtype), to_op(op), comm_, (hipStream_t)stream),
+         "ncclAllReduce");
   }
   void broadcast(uintptr_t ptr, size_t count, int dtype, int root, uintptr_t stream) {
-    nccl_check(ncclBroadcast((const void*)ptr, (void*)ptr, count, to_dtype(dtype), root, comm_, (hipStream_t)stream),
-               "ncclBroadcast");
+    call(ncclBroadcast((const void*)ptr, (void*)ptr, count, to_dtype(dtype), root, comm_, (hipStream_t)stream),
+         "ncclBroadcast");
   }
   void allgather(uintptr_t send, uintptr_t recv, size_t count, int dtype, uintptr_t stream) {
-    nccl_check(ncclAllGather((const void*)send, (void*)recv, count, to_dtype(dtype), comm_, (hipStream_t)stream),
-               "ncclAllGather");
+    call(ncclAllGather((const void*)send, (void*)recv, count, to_dtype(dtype), comm_, (hipStream_t)stream),
+         "ncclAllGather");
   }
   void reduce_scatter(uintptr_t send, uintptr_t recv, size_t count, int dtype, int op, uintptr_t stream) {
-    nccl_check(ncclReduceScatter((const void*)send, (void*)recv, count, to_dtype(dtype), to_op(op), comm_,
-                                 (hipStream_t)stream),
-               "ncclReduceScatter");
+    call(ncclReduceScatter((const void*)send, (void*)recv, count, to_dtype(dtype), to_op(op), comm_,
+                           (hipStream_t)stream),
+         "ncclReduceScatter");
   }
   std::string async_error() {
     ncclResult_t r = ncclSuccess;
@@ -119,8 +150,25 @@ class RcclComm {
   int world() const { return world_; }
 
  private:
+  // Poll the communicator's state until it leaves ncclInProgress; bounded by timeout_.
+  void settle(const char* what) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      ncclResult_t st = ncclSuccess;
+      nccl_check(ncclCommGetAsyncError(comm_, &st), "ncclCommGetAsyncError");
+      if (st != ncclInProgress) {
+        nccl_check(st, what);
+        return;
+      }
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_)
+        throw std::runtime_error(std::string(what) + ": timed out after " + std::to_string(timeout_) +
+                                 " s (did every rank join?)");
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+  }
   ncclComm_t comm_ = nullptr;
   int rank_, world_, device_;
+  double timeout_;
 };
 
 // Bucketed gradient all-reduce over RCCL.  The readiness logic lives in
@@ -185,7 +233,7 @@ class BucketReducer {
     const auto& ss = sched_.streams(b);
     for (int i = 0; i < (int)ss.size(); ++i)
       hip_check(hipStreamWaitEvent(comm_stream_, ev_[(size_t)b * BucketSchedule::kMaxStreams + i], 0), "wait bucket");
-    nccl_check(ncclAllReduce(arena_ + off_[b], arena_ + off_[b], cnt_[b], ncclFloat32, ncclSum, comm_.raw(),
+    comm_.call(ncclAllReduce(arena_ + off_[b], arena_ + off_[b], cnt_[b], ncclFloat32, ncclSum, comm_.raw(),
                              comm_stream_),
                "bucket allreduce");
     launched_.push_back(b);
@@ -241,7 +289,13 @@ class FakeCluster {
       ++gen_;
       cv_.notify_all();
     } else if (!cv_.wait_for(lk, std::chrono::duration<double>(timeout_), [&] { return gen_ != gen; })) {
-      err_ = "collective #" + std::to_string(seq_) + " timed out: ranks issued different collective sequences";
+      if (err_.empty())
+        err_ = "collective #" + std::to_string(seq_) + " timed out: ranks issued different collective sequences";
+      // the cluster stays poisoned with this FIRST error; reset the rendezvous so no later call reports a
+      // stale 'entered twice' instead of it
+      arrived_ = 0;
+      std::fill(in_.begin(), in_.end(), 0);
+      ++gen_;
       cv_.notify_all();
     }
     if (!err_.empty()) throw std::runtime_error(err_);
@@ -317,9 +371,10 @@ void register_rccl(py::module_& m) {
   py::class_<RcclComm>(m, "RcclComm")
       // uid arrives as std::string: converted from bytes BEFORE the GIL is
       // released (ncclCommInitRank blocks until every rank has joined)
-      .def(py::init([](int rank, int world, std::string uid, int device) {
-             return new RcclComm(rank, world, uid, device);
+      .def(py::init([](int rank, int world, std::string uid, int device, double init_timeout_s) {
+             return new RcclComm(rank, world, uid, device, init_timeout_s);
            }),
+           py::arg("rank"), py::arg("world"), py::arg("uid"), py::arg("device"), py::arg("init_timeout_s") = 300.0,
            py::call_guard<py::gil_scoped_release>())
       .def("allreduce", &RcclComm::allreduce)
       .def("broadcast", &RcclComm::broadcast)

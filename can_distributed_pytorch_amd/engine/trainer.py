@@ -73,9 +73,9 @@ class TorchStepper:
 
 
 class Fp32Stepper(TorchStepper):
-    """fp32 training numerics (the reference's, train.py:126) on the native kernels: every convolution —
-    forward, data and weight gradient — runs as split-bf16 GEMMs on the MFMA conv kernels with fp32
-    accumulation (ops/fp32.py); ReLU / pooling / the context module's elementwise math, the loss, DDP and SGD
+    """Approximately-fp32 training numerics (the reference trains fp32, train.py:126) on the native kernels: every
+    convolution — forward, data and weight gradient — runs as split-bf16 GEMMs on the MFMA conv kernels with fp32
+    accumulation (ops/fp32.py: ~2^-16 relative error per product, not bitwise fp32); ReLU / pooling / the context module's elementwise math, the loss, DDP and SGD
     are the fp32 ATen / torch.distributed ones of TorchStepper."""
     exec_backend = "hip_fp32"
 

@@ -15,7 +15,9 @@ with fp32 accumulation, in ONE launch of the bf16 kernels:
   dY = [hi; hi; lo], X = [hi; lo; hi], split_x3 mode 1) into the existing weight-gradient kernels, which
   accumulate and reduce in fp32; the bias gradient is an fp32 column sum of dY (bias_rows_reduce).
 
-Relative error of a product term is ~2^-17 (vs fp32's 2^-24 and TF32's 2^-11).  Everything between the
+Relative error of a product term is ~2^-16..2^-17 (vs fp32's 2^-24 and TF32's 2^-11): the operands carry about
+16 significant bits (lo is itself rounded to bf16) and lo*lo is dropped, so this is APPROXIMATELY fp32 — gradients
+can differ from true fp32 by ~1e-5 relative — not the reference's fp32 numerics bit for bit (parity unpinned).  Everything between the
 convolutions (ReLU, max-pool, the context module's pooling / upsampling / sigmoid weighting, the loss) stays
 fp32 in ATen, on channels-last (NHWC) tensors so the conv operands need no layout copies.
 

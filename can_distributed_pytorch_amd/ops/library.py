@@ -13,15 +13,16 @@ GPU — and an autograd formula built from the native backward kernels.
       kernel with the flipped / transposed weight pack, the weight + bias gradients on the split-pixel weight-
       gradient kernels (fp32, deterministic slab reduction) — the reference's nn.Conv2d + ReLU
       (model/CANNet.py:14-17, 114-115) as one op.
-  cannet::max_pool2x2(x) -> (y, codes)
-      2x2 / stride-2 max-pool of a non-negative (post-ReLU) NHWC map; codes = int32 first-max one-hots
-      (4 bits per channel).  Backward scatters through the codes (zero where the window max is 0, i.e. the
-      ReLU mask of the pool input is included).
+  cannet::relu_max_pool2x2(x) -> (y, codes)
+      the ReLU-fused 2x2 / stride-2 max-pool of an NHWC map: y = max_pool2d(relu(x), 2) (= relu of the window
+      max); codes = int32 first-max one-hots (4 bits per channel, 0 where the window max is <= 0).  Backward
+      scatters through the codes, so the ReLU's mask is part of the gradient: exactly the gradient of
+      max_pool2d(relu(x)), and of a plain max-pool only where the input is already non-negative.
   cannet::sgd_momentum_(param, momentum_buf, grad, lr, momentum, grad_scale) -> ()
       in-place fused SGD with momentum on contiguous fp32 tensors (torch.optim.SGD semantics, weight decay 0,
       dampening 0: buf = momentum * buf + grad_scale * grad; param -= lr * buf), one kernel.
 
-``Conv2dNHWC`` / ``MaxPool2x2`` are nn.Module wrappers with fp32 master parameters.
+``Conv2dNHWC`` / ``ReluMaxPool2x2`` are nn.Module wrappers with fp32 master parameters.
 """
 from __future__ import annotations
 
@@ -116,12 +117,13 @@ def _conv_bwd(ctx, dy):
 conv2d_nhwc.register_autograd(_conv_bwd, setup_context=_conv_setup)
 
 
-@torch.library.custom_op(f"{_LIB}::max_pool2x2", mutates_args=())
-def max_pool2x2(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-    return C.maxpool_codes(x.contiguous())
+@torch.library.custom_op(f"{_LIB}::relu_max_pool2x2", mutates_args=())
+def relu_max_pool2x2(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    y, codes = C.maxpool_codes(x.contiguous())
+    return y.clamp_min_(0), codes          # relu(max): a window whose max is <= 0 pools to 0 (its code is 0)
 
 
-@max_pool2x2.register_fake
+@relu_max_pool2x2.register_fake
 def _(x):
     n, h, w, c = x.shape
     if h % 2 or w % 2 or c % 8:
@@ -129,12 +131,12 @@ def _(x):
     return x.new_empty(n, h // 2, w // 2, c), x.new_empty(n, h // 2, w // 2, c // 8, dtype=torch.int32)
 
 
-@torch.library.custom_op(f"{_LIB}::max_pool2x2_backward", mutates_args=())
-def max_pool2x2_backward(dy: torch.Tensor, codes: torch.Tensor) -> torch.Tensor:
+@torch.library.custom_op(f"{_LIB}::relu_max_pool2x2_backward", mutates_args=())
+def relu_max_pool2x2_backward(dy: torch.Tensor, codes: torch.Tensor) -> torch.Tensor:
     return C.maxpool_bwd_codes(codes, dy.contiguous())
 
 
-@max_pool2x2_backward.register_fake
+@relu_max_pool2x2_backward.register_fake
 def _(dy, codes):
     n, h, w, c = dy.shape
     return dy.new_empty(n, 2 * h, 2 * w, c)
@@ -147,10 +149,10 @@ def _pool_setup(ctx, inputs, output):
 
 def _pool_bwd(ctx, dy, dcodes):
     (codes,) = ctx.saved_tensors
-    return max_pool2x2_backward(dy, codes)
+    return relu_max_pool2x2_backward(dy, codes)
 
 
-max_pool2x2.register_autograd(_pool_bwd, setup_context=_pool_setup)
+relu_max_pool2x2.register_autograd(_pool_bwd, setup_context=_pool_setup)
 
 
 @torch.library.custom_op(f"{_LIB}::sgd_momentum_", mutates_args=("param", "momentum_buf"))
@@ -204,8 +206,9 @@ class Conv2dNHWC(nn.Module):
         return torch.ops.cannet.conv2d_nhwc(x, self.weight, self.bias, self.dilation, self.relu)
 
 
-class MaxPool2x2(nn.Module):
-    """2x2 / stride-2 max-pool of a post-ReLU NHWC map (``torch.ops.cannet.max_pool2x2``)."""
+class ReluMaxPool2x2(nn.Module):
+    """ReLU followed by a 2x2 / stride-2 max-pool of an NHWC map, as one op (``torch.ops.cannet.relu_max_pool2x2``);
+    after a ReLU (Conv2dNHWC(relu=True)) it is the plain max-pool."""
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return torch.ops.cannet.max_pool2x2(x)[0]
+        return torch.ops.cannet.relu_max_pool2x2(x)[0]

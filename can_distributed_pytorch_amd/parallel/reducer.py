@@ -115,14 +115,19 @@ class BucketedReducer:
         self._works = []
 
     def _make_comm_agreed(self, dev, group):
-        """This rank's RCCL communicator, or None on EVERY rank if any rank failed to create one: the ranks
-        agree through one all-reduce on the torch process group, and the reducer then runs its buckets through
-        torch.distributed (the same RCCL underneath, without the owned communicator) instead of training
-        with mismatched transports."""
+        """This rank's RCCL communicator, or None on EVERY rank if any rank failed to create one.  Every step
+        that can fail is bounded and followed by a step every rank reaches, so a failure on one rank cannot strand
+        the others in a blocking call:
+          1. rank 0 broadcasts (ok, unique id | error) — a failed ncclGetUniqueId is seen by every rank;
+          2. the communicator is initialised NON-blocking with a deadline (csrc/rccl_reducer.cpp: RcclComm), so
+             ranks whose peer died before or inside its init time out and return instead of waiting forever;
+          3. one all-reduce of a failure flag on the torch process group: if any rank failed, every rank aborts
+             its communicator and the reducer runs its buckets through torch.distributed (the same RCCL
+             underneath, without the owned communicator) instead of training with mismatched transports."""
         comm, err = None, None
         try:
             comm = make_rccl_comm(dev, group)
-        except RuntimeError as e:                 # e.g. communicator init refused by RCCL
+        except Exception as e:                    # any failure, not only RCCL's RuntimeError
             err = e
         if self.world > 1:
             ok = torch.tensor([0.0 if err is None else 1.0], device=dev)
@@ -131,6 +136,8 @@ class BucketedReducer:
         else:
             failed = err is not None
         if failed:
+            if comm is not None:
+                comm.abort()
             import warnings
             warnings.warn(f"owned RCCL communicator unavailable ({err or 'failed on another rank'}); "
                           "gradient buckets go through torch.distributed")
@@ -214,15 +221,28 @@ class BucketedReducer:
         return handles
 
 
-def make_rccl_comm(device, group=None):
-    """Create this process's RCCL communicator; the 128-byte unique id travels
-    through the existing torch process group (one broadcast_object_list)."""
+def make_rccl_comm(device, group=None, init_timeout_s: Optional[float] = None):
+    """Create this process's RCCL communicator; the 128-byte unique id travels through the existing torch process
+    group (one broadcast_object_list) together with rank 0's ok flag, so a rank-0 failure to make the id raises on
+    every rank.  The init itself is bounded by ``init_timeout_s`` (env CANNET_RCCL_INIT_TIMEOUT, default 300 s)."""
+    import os
     from ..ops import _ext
     C = _ext.require()
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     world = dist.get_world_size(group) if dist.is_initialized() else 1
-    obj = [C.rccl_unique_id() if rank == 0 else None]
+    if init_timeout_s is None:
+        init_timeout_s = float(os.environ.get("CANNET_RCCL_INIT_TIMEOUT", "300"))
+    msg = None
+    if rank == 0:
+        try:
+            msg = (True, C.rccl_unique_id())
+        except Exception as e:
+            msg = (False, f"rank 0: ncclGetUniqueId failed: {e}")
+    obj = [msg]
     if world > 1:
         dist.broadcast_object_list(obj, src=0, group=group)
+    ok, payload = obj[0]
+    if not ok:
+        raise RuntimeError(payload)
     dev = torch.device(device)
-    return C.RcclComm(rank, world, obj[0], dev.index if dev.index is not None else 0)
+    return C.RcclComm(rank, world, payload, dev.index if dev.index is not None else 0, float(init_timeout_s))

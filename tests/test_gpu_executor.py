@@ -241,3 +241,17 @@ def test_native_stepper_w1g_fused_matches_default(monkeypatch):
         assert abs(u - v) <= 1e-3 * abs(u), (la, lb)
     for (name, p0), pa, pb in zip(init, nat_a.parameters(), nat_b.parameters()):
         assert _rel(pb - p0, pa - p0) < 1e-2, name
+
+
+def test_rccl_comm_init_is_bounded_when_a_peer_never_joins():
+    """The owned communicator initialises non-blocking with a deadline: a 2-rank communicator whose second rank
+    never joins raises after the timeout (and aborts the half-made communicator) instead of blocking forever —
+    the property parallel/reducer.py's fall-back agreement relies on."""
+    import time
+    from can_distributed_pytorch_amd.ops import _ext
+    C = _ext.require()
+    uid = C.rccl_unique_id()
+    t0 = time.perf_counter()
+    with pytest.raises(RuntimeError, match="timed out"):
+        C.RcclComm(0, 2, uid, torch.cuda.current_device(), 3.0)
+    assert time.perf_counter() - t0 < 60

@@ -45,3 +45,24 @@ def test_train_and_test_py_native(tmp_path):
                          str(ck / best[-1]), "--show", "0"], capture_output=True, text=True, timeout=300,
                         cwd=str(tmp_path))
     assert r2.returncode == 0 and "mae:" in r2.stdout, r2.stderr[-3000:]
+
+
+def test_train_py_hip_fp32_save_and_resume(tmp_path):
+    """--impl hip --dtype fp32 runs the split-bf16 Fp32Stepper (a TorchStepper): the epoch loop, the lr
+    schedule, last_state.pth (torch optimizer momentum) and --resume must all take the torch-optimizer branch."""
+    data = tmp_path / "data"
+    _make_dataset(str(data))
+    ck = tmp_path / "ck"
+    base = [sys.executable, os.path.join(ROOT, "train.py"), "--data_root", str(data), "--batch-size", "1",
+            "--num-workers", "0", "--wandb", "false", "--show", "false", "--lr", "1e-6", "--impl", "hip",
+            "--dtype", "fp32", "--lr-schedule", "cosine", "--checkpoint-dir", str(ck),
+            "--log-jsonl", str(ck / "metrics.jsonl")]
+    r = subprocess.run(base + ["--epochs", "1"], capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    assert os.path.exists(ck / "last_state.pth")
+    r = subprocess.run(base + ["--epochs", "2", "--resume", str(ck / "last_state.pth")], capture_output=True,
+                       text=True, timeout=600, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    ep = [json.loads(x) for x in open(ck / "metrics.jsonl")]
+    ep = [x for x in ep if x["kind"] == "epoch"]
+    assert [x["epoch"] for x in ep] == [0, 1] and all(np.isfinite(x["loss"]) for x in ep)

@@ -8,7 +8,7 @@ from can_distributed_pytorch_amd.ops import library as L  # noqa: F401  (registe
 
 
 def test_ops_registered():
-    for name in ("conv2d_nhwc", "conv2d_nhwc_backward", "max_pool2x2", "max_pool2x2_backward", "sgd_momentum_"):
+    for name in ("conv2d_nhwc", "conv2d_nhwc_backward", "relu_max_pool2x2", "relu_max_pool2x2_backward", "sgd_momentum_"):
         assert hasattr(torch.ops.cannet, name)
 
 
@@ -20,7 +20,7 @@ def test_fake_shapes_cpu():
         b = torch.empty(64)
         y = torch.ops.cannet.conv2d_nhwc(x, w, b, 2, True)
         assert y.shape == (2, 24, 32, 64) and y.dtype == torch.bfloat16
-        p, codes = torch.ops.cannet.max_pool2x2(y)
+        p, codes = torch.ops.cannet.relu_max_pool2x2(y)
         assert p.shape == (2, 12, 16, 64) and codes.shape == (2, 12, 16, 8) and codes.dtype == torch.int32
         dx, dw, db = torch.ops.cannet.conv2d_nhwc_backward(y, x, y, w, 2, True, True)
         assert dx.shape == x.shape and dw.shape == w.shape and db.shape == (64,)
@@ -87,7 +87,7 @@ def test_maxpool_op_vs_aten():
     torch.manual_seed(1)
     x = F.relu(torch.randn(2, 16, 24, 64, device="cuda")).to(torch.bfloat16)
     xg = x.clone().requires_grad_(True)
-    y = L.MaxPool2x2()(xg)
+    y = L.ReluMaxPool2x2()(xg)
     xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
     yr = F.relu(F.max_pool2d(xr, 2, 2))
     assert torch.equal(y.float().permute(0, 3, 1, 2), yr)
@@ -95,6 +95,24 @@ def test_maxpool_op_vs_aten():
     yr.backward(g)
     y.backward(g.permute(0, 2, 3, 1).to(torch.bfloat16))
     assert _rel(xg.grad.float().permute(0, 3, 1, 2), xr.grad) < 1e-2
+
+
+@pytest.mark.gpu
+def test_relu_maxpool_op_signed_input_vs_aten():
+    """Signed input (no ReLU before the op): values and gradient are those of max_pool2d(relu(x))."""
+    torch.manual_seed(3)
+    x = torch.randn(2, 10, 14, 64, device="cuda").to(torch.bfloat16)
+    x[0, :2, :2, :8] = -1.0                       # whole windows <= 0
+    xg = x.clone().requires_grad_(True)
+    y = L.ReluMaxPool2x2()(xg)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.max_pool2d(F.relu(xr), 2, 2)
+    assert torch.equal(y.float().permute(0, 3, 1, 2), yr)
+    g = torch.randn_like(yr)
+    yr.backward(g)
+    y.backward(g.permute(0, 2, 3, 1).to(torch.bfloat16))
+    assert _rel(xg.grad.float().permute(0, 3, 1, 2), xr.grad) < 1e-2
+    assert torch.count_nonzero(xg.grad[0, :2, :2, :8]) == 0
 
 
 @pytest.mark.gpu
@@ -124,7 +142,7 @@ def test_opcheck_conv():
 
 @pytest.mark.gpu
 def test_compile_fullgraph():
-    m = torch.nn.Sequential(L.Conv2dNHWC(64, 64), L.MaxPool2x2(), L.Conv2dNHWC(64, 128)).cuda()
+    m = torch.nn.Sequential(L.Conv2dNHWC(64, 64), L.ReluMaxPool2x2(), L.Conv2dNHWC(64, 128)).cuda()
     x = torch.randn(2, 16, 32, 64, device="cuda").to(torch.bfloat16)
     ref = m(x)
     out = torch.compile(m, fullgraph=True, backend="aot_eager")(x)

@@ -130,3 +130,61 @@ def _consistency_case(rank, world):
 
 def test_replica_desync_detection_gloo():
     _run(_consistency_case, 2)
+
+
+class _FakeExt:
+    """Stands in for the native extension inside a spawned rank: scripted unique-id / communicator failures."""
+
+    def __init__(self, rank, uid_fails=False, init_fails_on=None):
+        self.rank, self.uid_fails, self.init_fails_on = rank, uid_fails, init_fails_on
+        self.made = []
+
+    def rccl_unique_id(self):
+        if self.uid_fails:
+            raise OSError("no network interface for the bootstrap")
+        return b"\0" * 128
+
+    def RcclComm(self, rank, world, uid, device, timeout):
+        if rank == self.init_fails_on:
+            raise ValueError("scripted init failure (not a RuntimeError)")
+        ext = self
+
+        class _Comm:
+            aborted = False
+
+            def abort(self):
+                _Comm.aborted = True
+        c = _Comm()
+        ext.made.append(c)
+        return c
+
+
+def _comm_agreement_case(rank, world, uid_fails, init_fails_on):
+    """Every rank returns from reducer construction (no rank stranded in a blocking call) and every rank falls back
+    to the torch transport together; a communicator that did get made on a healthy rank is aborted."""
+    import warnings
+    from can_distributed_pytorch_amd.ops import _ext
+    from can_distributed_pytorch_amd.parallel import reducer as R
+    from can_distributed_pytorch_amd.utils.flat import FlatArena
+    fake = _FakeExt(rank, uid_fails=uid_fails, init_fails_on=init_fails_on)
+    _ext.require = lambda: fake
+    params = [torch.nn.Parameter(torch.zeros(100)), torch.nn.Parameter(torch.zeros(10))]
+    arena = FlatArena(params, "cpu", order=[1, 0])
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        red = R.BucketedReducer(arena, [1, 0], bucket_mb=1.0, transport="rccl")
+    assert red.transport == "torch" and red._native is None
+    assert all(c.aborted for c in fake.made)
+    if not uid_fails and rank != init_fails_on:
+        assert len(fake.made) == 1                 # this rank's own init succeeded, then it was aborted
+    for g in arena.grad_views():
+        g.fill_(rank + 1.0)
+    red.begin()
+    red.mark_ready([1, 0])
+    red.finish()                                   # the fallback transport really reduces
+    assert all(torch.all(g == sum(r + 1.0 for r in range(world))) for g in arena.grad_views())
+
+
+@pytest.mark.parametrize("uid_fails,init_fails_on", [(True, None), (False, 1), (False, 0)])
+def test_rccl_comm_failure_agreement_multirank(uid_fails, init_fails_on):
+    _run(_comm_agreement_case, 3, uid_fails, init_fails_on)

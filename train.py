@@ -167,7 +167,10 @@ def main(args):
     from can_distributed_pytorch_amd.engine.trainer import build_trainer
     fixed = bool(args.synthetic)
     graph = bool(args.graph) and fixed
-    if args.impl == "hip" and args.dtype != "fp32":
+    # the fused native stepper (flat arena, RCCL reducer, device lr) runs --impl hip in bf16 / fp16; every other
+    # combination (--impl torch, and --impl hip --dtype fp32 = Fp32Stepper) is a TorchStepper with a torch optimizer
+    native = args.impl == "hip" and args.dtype != "fp32"
+    if native:
         stepper = build_trainer(impl="hip", dtype=args.dtype, device=device, world=world, lr=base_lr, graph=graph,
                                 model=model, bucket_mb=args.bucket_mb)
         net = stepper.model
@@ -186,9 +189,9 @@ def main(args):
     start_epoch, min_mae, min_epoch = 0, float("inf"), 0
     if args.resume and os.path.exists(args.resume):
         rs = load_train_state(args.resume, stepper.model, momentum,
-                              optimizer=None if args.impl == "hip" else stepper.opt)
+                              optimizer=None if native else stepper.opt)
         start_epoch, min_mae, min_epoch = rs["epoch"] + 1, rs["min_mae"], rs["min_epoch"]
-        if args.impl == "hip":
+        if native:
             stepper.load_resume_state(rs["stepper"])
 
     from can_distributed_pytorch_amd.engine.train_eval import train_one_epoch_native, evaluate, train_one_epoch
@@ -197,13 +200,13 @@ def main(args):
         train_sampler.set_epoch(epoch)
         if args.lr_schedule == "cosine":
             f = ((1 + math.cos(epoch * math.pi / args.epochs)) / 2) * (1 - args.lrf) + args.lrf
-            if args.impl == "hip":
+            if native:
                 stepper.lr = base_lr * world * f
             else:
                 for g in stepper.opt.param_groups:
                     g["lr"] = base_lr * world * f
         t0 = time.perf_counter()
-        if args.impl == "hip":
+        if native:
             mean_loss = train_one_epoch_native(stepper, train_loader, device, epoch, log=log, prep=prep)
         else:
             mean_loss = train_one_epoch(net, stepper.opt, train_loader, device, epoch)
@@ -215,7 +218,7 @@ def main(args):
             mae_sum = float("nan")
         if args.check_sync_every and (epoch + 1) % args.check_sync_every == 0 and world > 1:
             from can_distributed_pytorch_amd.parallel.consistency import check_replicas_consistent, check_comm_health
-            if args.impl == "hip":
+            if native:
                 check_comm_health(stepper.reducer)
                 check_replicas_consistent(stepper.arena.data)
             else:
@@ -226,9 +229,9 @@ def main(args):
                 min_mae, min_epoch = mean_mae, epoch
                 save_checkpoint(stepper.model, os.path.join(args.checkpoint_dir, f"epoch_{epoch}.pth"))
             save_train_state(os.path.join(args.checkpoint_dir, "last_state.pth"), stepper.model, momentum, epoch,
-                             min_mae, optimizer=None if args.impl == "hip" else stepper.opt, min_epoch=min_epoch,
-                             stepper_state=stepper.resume_state() if args.impl == "hip" else None)
-            lr_now = stepper.lr if args.impl == "hip" else stepper.opt.param_groups[0]["lr"]
+                             min_mae, optimizer=None if native else stepper.opt, min_epoch=min_epoch,
+                             stepper_state=stepper.resume_state() if native else None)
+            lr_now = stepper.lr if native else stepper.opt.param_groups[0]["lr"]
             ips = len(train_loader) * args.batch_size * world / max(t_train, 1e-9)
             print(f"[epoch {epoch}] loss: {mean_loss:.4f} mae: {mean_mae:.3f}, min_mae: {min_mae:.3f}, "
                   f"min_epoch: {min_epoch}, train img/s {ips:.1f}")
