@@ -74,6 +74,13 @@ int can_ctx_bwd_e1(const void* dcat, const void* ws, const float* T, void* dz, v
                    int dt, void* stream);
 int can_ctx_gemm(int mode, const float* x, const float* y, const float* const* w, float* out, float* const* gw, int N,
                  int C, float beta, float scale, const float* dscale, void* stream);
+// linearised context module (conv_igemm.hip EPI_CTXF / EPI_CTXB + context.hip ctx_bwd_lin)
+int can_conv_ctx(int fwd, const void* x, const void* w, const float* tab0, const float* tab1, const void* fv, void* cat,
+                 void* y, int N, int H, int W, int C, int dt, void* stream);
+int can_ctx_bwd_lin(const void* dcat, const void* wts, const float* U, void* dg, float* rowacc, int N, int h, int w,
+                    int C, int dt, void* stream);
+int can_ctx_cells(const float* rowacc, float* cells, int N, int h, int C, void* stream);
+int can_ctx_w2_scatter(const float* tmp, float* const* dst, int C, float beta, void* stream);
 int can_ctx_bwd_final(const void* dcat, const void* dc, const float* dave, const void* fv, void* dfv, int N, int h,
                       int w, int C, int dt, void* stream);
 

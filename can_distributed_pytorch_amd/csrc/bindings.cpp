@@ -210,6 +210,25 @@ PYBIND11_MODULE(CAN_MODULE_NAME, m) {
                        (const float*)dscale, P(st)),
           "ctx_gemm");
   });
+  m.def("conv_ctx", [](int fwd, uintptr_t x, uintptr_t w, uintptr_t tab0, uintptr_t tab1, uintptr_t fv, uintptr_t cat,
+                       uintptr_t y, int N, int H, int W, int C, int dt, uintptr_t st) {
+    check(can_conv_ctx(fwd, P(x), P(w), (const float*)tab0, (const float*)tab1, P(fv), P(cat), P(y), N, H, W, C, dt,
+                       P(st)),
+          "conv_ctx");
+  });
+  m.def("ctx_bwd_lin", [](uintptr_t dcat, uintptr_t wts, uintptr_t U, uintptr_t dg, uintptr_t rowacc, int N, int h,
+                          int w, int C, int dt, uintptr_t st) {
+    check(can_ctx_bwd_lin(P(dcat), P(wts), (const float*)U, P(dg), (float*)rowacc, N, h, w, C, dt, P(st)),
+          "ctx_bwd_lin");
+  });
+  m.def("ctx_cells", [](uintptr_t rowacc, uintptr_t cells, int N, int h, int C, uintptr_t st) {
+    check(can_ctx_cells((const float*)rowacc, (float*)cells, N, h, C, P(st)), "ctx_cells");
+  });
+  m.def("ctx_w2_scatter", [](uintptr_t tmp, std::vector<uintptr_t> dst, int C, float beta, uintptr_t st) {
+    if (dst.size() != 4) throw std::runtime_error("ctx_w2_scatter: 4 scales");
+    float* d[4] = {(float*)dst[0], (float*)dst[1], (float*)dst[2], (float*)dst[3]};
+    check(can_ctx_w2_scatter((const float*)tmp, d, C, beta, P(st)), "ctx_w2_scatter");
+  });
   m.def("ctx_bwd_final", [](uintptr_t dcat, uintptr_t dc, uintptr_t dave, uintptr_t fv, uintptr_t dfv, int N, int h,
                             int w, int C, int dt, uintptr_t st) {
     check(can_ctx_bwd_final(P(dcat), P(dc), (const float*)dave, P(fv), P(dfv), N, h, w, C, dt, P(st)),

@@ -471,6 +471,157 @@ __global__ void __launch_bounds__(256) ctx_bwd_final_kernel(const uint4* __restr
 
 
 // ---------------------------------------------------------------------------
+// Backward of the linearised context module (conv_igemm.hip, EPI_CTXF: z_S = up(t_S) - G_S,
+// w_S = sigmoid(z_S), fi = sum_S w_S s_S / D, D = sum_S w_S + 1e-12, s_S = up(u_S)).  Per pixel and channel
+// from dfi = dcat[:, C:] and the saved w (fi and s_S are recomputed in fp32 from w and the u table):
+//   g = dfi / D,  dz_S = g (s_S - fi) w_S (1 - w_S),  ds_S = g w_S
+//   dG = -dz  -> dg [P][4C] (interleaved like w; the operand of the data / weight gradient GEMMs)
+//   up^T(dz_S) and up^T(ds_S) along x -> row partials rowacc[2][N*h][12][C] (y pass: ctx_cells_kernel)
+// Block = one image row x 128 channels; thread = (x segment, channel pair): a wave reads 64 consecutive
+// channel pairs of one pixel (256-B dfi, 1-KiB w / dg rows); the 4 segments of a row are summed through LDS
+// in a fixed order (deterministic).
+template <int DT>
+__global__ void __launch_bounds__(256) ctx_bwd_lin_kernel(const uint32_t* __restrict__ dcat,
+                                                          const uint4* __restrict__ wts, const float* __restrict__ U,
+                                                          uint4* __restrict__ dg, float* __restrict__ rowacc, int N,
+                                                          int h, int w, int C) {
+  __shared__ float red[4][64][49];                 // [segment][pair][12 bins x 2 tensors x 2 channels] (+1 pad)
+  const int ncb = C / 128;
+  const size_t ny = blockIdx.x / ncb;              // n*h + y
+  const int cbase = (blockIdx.x % ncb) * 128;
+  const int seg = threadIdx.x >> 6, cp = threadIdx.x & 63;
+  const int c = cbase + 2 * cp;
+  const int n = (int)(ny / h), y = (int)(ny - (size_t)n * h);
+  // y-interpolated u rows of the 12 column bins, this thread's two channels
+  float R[12][2];
+#pragma unroll
+  for (int si = 0; si < 4; ++si) {
+    const int S = (si == 0) ? 1 : (si == 1) ? 2 : (si == 2) ? 3 : 6;
+    const int bo = (si == 0) ? 0 : (si == 1) ? 1 : (si == 2) ? 3 : 6;
+    const int co = (si == 0) ? 0 : (si == 1) ? 1 : (si == 2) ? 5 : 14;
+    int y0, y1;
+    float ly;
+    bil(S, y, h, y0, y1, ly);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      if (j < S) {
+        const float2 a = *reinterpret_cast<const float2*>(U + ((size_t)n * 50 + co + y0 * S + j) * C + c);
+        const float2 b = *reinterpret_cast<const float2*>(U + ((size_t)n * 50 + co + y1 * S + j) * C + c);
+        R[bo + j][0] = (1.f - ly) * a.x + ly * b.x;
+        R[bo + j][1] = (1.f - ly) * a.y + ly * b.y;
+      }
+    }
+  }
+  float aT[12][2], aU[12][2];
+#pragma unroll
+  for (int b = 0; b < 12; ++b) { aT[b][0] = aT[b][1] = aU[b][0] = aU[b][1] = 0.f; }
+  const int xs = (w + 3) / 4;
+  const int x0 = seg * xs, x1 = min(w, x0 + xs);
+  const int C2 = C >> 1;                            // dcat words (2 channels) per C
+  for (int x = x0; x < x1; ++x) {
+    const size_t p = ny * w + x;
+    const uint32_t dw = dcat[p * C + C2 + (c >> 1)];          // dcat row = 2C elements = C words; fi half
+    const uint4 wq = wts[(p * 4 * C + 4 * c) >> 3];
+    float wv[8];
+    unpack8h<DT>(wq, wv);                                     // [ch0: S0..S3, ch1: S0..S3]
+    const float dfi[2] = {h2f<DT>((unsigned short)(dw & 0xffffu)), h2f<DT>((unsigned short)(dw >> 16))};
+    // x weights of the 12 bins
+    float wx[12];
+#pragma unroll
+    for (int si = 0; si < 4; ++si) {
+      const int S = (si == 0) ? 1 : (si == 1) ? 2 : (si == 2) ? 3 : 6;
+      const int bo = (si == 0) ? 0 : (si == 1) ? 1 : (si == 2) ? 3 : 6;
+      int xa, xb;
+      float lx;
+      bil(S, x, w, xa, xb, lx);
+#pragma unroll
+      for (int j = 0; j < 6; ++j)
+        if (j < S) wx[bo + j] = ((j == xa) ? 1.f - lx : 0.f) + ((j == xb) ? lx : 0.f);
+    }
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      float sS[4];
+      float num = 0.f, den = 0.f;
+#pragma unroll
+      for (int si = 0; si < 4; ++si) {
+        const int S = (si == 0) ? 1 : (si == 1) ? 2 : (si == 2) ? 3 : 6;
+        const int bo = (si == 0) ? 0 : (si == 1) ? 1 : (si == 2) ? 3 : 6;
+        float v = 0.f;
+#pragma unroll
+        for (int j = 0; j < 6; ++j)
+          if (j < S) v += wx[bo + j] * R[bo + j][k];
+        sS[si] = v;
+        const float ws = wv[4 * k + si];
+        num += ws * v;
+        den += ws;
+      }
+      const float rden = __builtin_amdgcn_rcpf(den + 1e-12f);     // v_rcp_f32 (1 ulp)
+      const float fi = num * rden;
+      const float g = dfi[k] * rden;
+#pragma unroll
+      for (int si = 0; si < 4; ++si) {
+        const int S = (si == 0) ? 1 : (si == 1) ? 2 : (si == 2) ? 3 : 6;
+        const int bo = (si == 0) ? 0 : (si == 1) ? 1 : (si == 2) ? 3 : 6;
+        const float ws = wv[4 * k + si];
+        const float dz = g * (sS[si] - fi) * ws * (1.f - ws);
+        const float ds = g * ws;
+        o[4 * k + si] = -dz;
+#pragma unroll
+        for (int j = 0; j < 6; ++j)
+          if (j < S) {
+            aT[bo + j][k] += wx[bo + j] * dz;
+            aU[bo + j][k] += wx[bo + j] * ds;
+          }
+      }
+    }
+    dg[(p * 4 * C + 4 * c) >> 3] = pack8h<DT>(o);
+  }
+  float* rr = &red[seg][cp][0];
+#pragma unroll
+  for (int b = 0; b < 12; ++b) {
+    rr[b * 4 + 0] = aT[b][0]; rr[b * 4 + 1] = aT[b][1];
+    rr[b * 4 + 2] = aU[b][0]; rr[b * 4 + 3] = aU[b][1];
+  }
+  __syncthreads();
+  // 256 threads store 64 pairs x 12 bins x 2 tensors: thread -> (pair, 3 bins)
+  const size_t P_ = (size_t)N * h;
+  for (int e = threadIdx.x; e < 64 * 12; e += 256) {
+    const int pr = e & 63, b = e >> 6;
+    float t0 = 0.f, t1 = 0.f, u0 = 0.f, u1 = 0.f;
+#pragma unroll
+    for (int sg = 0; sg < 4; ++sg) {
+      t0 += red[sg][pr][b * 4 + 0]; t1 += red[sg][pr][b * 4 + 1];
+      u0 += red[sg][pr][b * 4 + 2]; u1 += red[sg][pr][b * 4 + 3];
+    }
+    const size_t o0 = (ny * 12 + b) * C + cbase + 2 * pr;
+    *reinterpret_cast<float2*>(rowacc + o0) = make_float2(t0, t1);
+    *reinterpret_cast<float2*>(rowacc + P_ * 12 * C + o0) = make_float2(u0, u1);
+  }
+}
+
+// dW2_S[c][k] = beta * dW2_S[c][k] + tmp[4c + si][k]: the interleaved rows of the linearised weight gradient
+// (W2cat = rows 4c + si) back into the four conv{S}_2 weights
+__global__ void __launch_bounds__(256) ctx_w2_scatter_kernel(const float4* __restrict__ tmp, float* d0, float* d1,
+                                                             float* d2, float* d3, int C, float beta) {
+  const int C4 = C >> 2;
+  const size_t total = (size_t)4 * C * C4;
+  for (size_t t = blockIdx.x * 256 + threadIdx.x; t < total; t += (size_t)gridDim.x * 256) {
+    const int k4 = (int)(t % C4);
+    const size_t row = t / C4;                      // 4c + si
+    const int si = (int)(row & 3), c = (int)(row >> 2);
+    float* d = (si == 0) ? d0 : (si == 1) ? d1 : (si == 2) ? d2 : d3;
+    float4* o = reinterpret_cast<float4*>(d + (size_t)c * C) + k4;
+    float4 v = tmp[t];
+    if (beta != 0.f) {
+      const float4 q = *o;
+      v.x += beta * q.x; v.y += beta * q.y; v.z += beta * q.z; v.w += beta * q.w;
+    }
+    *o = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // conv{S}_1 (1x1, 512->512, no bias) on the pooled S x S grids, all four
 // scales in ONE launch (blockIdx.z = scale), fp32 (model/CANNet.py:43,52,61,72;
 // SURVEY §2.5 X2).  Cells are [N][50][C] fp32 (scale S at cell offset
@@ -601,8 +752,13 @@ __global__ void __launch_bounds__(256) ctx_gemm_kernel(CtxGemmArgs a) {
       }
       *reinterpret_cast<float4*>(g) = o;
     } else {
-      *reinterpret_cast<float4*>(a.out + (size_t)ctx_cell_row(m, k2, off) * C + n) =
-          make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+      float* o = a.out + (size_t)ctx_cell_row(m, k2, off) * C + n;
+      float4 v = make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+      if (a.beta != 0.f) {
+        const float4 p = *reinterpret_cast<const float4*>(o);
+        v.x += a.beta * p.x; v.y += a.beta * p.y; v.z += a.beta * p.z; v.w += a.beta * p.w;
+      }
+      *reinterpret_cast<float4*>(o) = v;
     }
   }
 }
@@ -646,6 +802,30 @@ extern "C" int can_ctx_reduce(int mode, const void* in0, const void* sdir, const
 }
 
 static inline dim3 ctx_grid(int N, int h, int C) { return dim3(N * h * ((C / 8 + 63) / 64) * 2); }
+
+extern "C" int can_ctx_bwd_lin(const void* dcat, const void* wts, const float* U, void* dg, float* rowacc, int N,
+                               int h, int w, int C, int dt, void* stream) {
+  if (C % 128) return -2;
+  CAN_LAUNCH_DT(dt, ctx_bwd_lin_kernel, dim3(N * h * (C / 128)), dim3(256), 0, (hipStream_t)stream,
+                (const uint32_t*)dcat, (const uint4*)wts, U, (uint4*)dg, rowacc, N, h, w, C);
+  return (int)hipGetLastError();
+}
+
+// y pass of the separable bilinear adjoint only: rowacc [N][h][12][C] -> cells [N][50][C]
+extern "C" int can_ctx_cells(const float* rowacc, float* cells, int N, int h, int C, void* stream) {
+  const size_t tc = (size_t)N * 50 * C;
+  hipLaunchKernelGGL(ctx_cells_kernel<false>, dim3(gridn(tc)), dim3(256), 0, (hipStream_t)stream, rowacc, cells, N, h,
+                     C);
+  return (int)hipGetLastError();
+}
+
+extern "C" int can_ctx_w2_scatter(const float* tmp, float* const* dst, int C, float beta, void* stream) {
+  if (C % 4) return -2;
+  const size_t total = (size_t)C * C;             // float4 items = 4C rows x C/4
+  hipLaunchKernelGGL(ctx_w2_scatter_kernel, dim3(gridn(total, 2048)), dim3(256), 0, (hipStream_t)stream,
+                     (const float4*)tmp, dst[0], dst[1], dst[2], dst[3], C, beta);
+  return (int)hipGetLastError();
+}
 
 extern "C" int can_ctx_expand(const void* fv, const float* T, void* cs, int N, int h, int w, int C, int dt,
                               void* stream) {

@@ -60,8 +60,10 @@ struct ConvArgs {
 // EPI_F32 (LDS-DMA kernels only): the raw GEMM result (+ bias when a.bias is given) stored as fp32 into
 // a.y reinterpreted as float [M][Cout] — the split-bf16 fp32 path (ops/fp32.py) sums hi*hi + hi*lo + lo*hi
 // in one K-concatenated GEMM and needs the fp32 accumulator, not its 16-bit rounding.
+// EPI_CTXF / EPI_CTXB (LDS-DMA v2 kernel, 256 x 256 tiles, 1x1): the context module as ONE GEMM each way,
+// see "Linearised context module" below.
 enum { EPI_BIAS_RELU = 0, EPI_MASK = 1, EPI_NONE = 2, EPI_BIAS = 3, EPI_SIGMOID = 4, EPI_POOLBWD = 5,
-       EPI_POOLFWD = 6, EPI_F32 = 7 };
+       EPI_POOLFWD = 6, EPI_F32 = 7, EPI_CTXF = 8, EPI_CTXB = 9 };
 enum { LOAD_GENERIC = 0, LOAD_FIRST = 1 };
 
 
@@ -323,6 +325,13 @@ struct ConvArgs2 {
   float* bpart = nullptr;
   // batched launch (v2 kernel): item blockIdx.y reads x + y*xbs, w + y*wbs and writes y + y*ybs (elements)
   long long xbs = 0, wbs = 0, ybs = 0;
+  // EPI_CTXF / EPI_CTXB: context-module cell tables [N][50][cC] fp32 (CTXF: ctab0 = t = W2 u, ctab1 = u = W1 ave;
+  // CTXB: ctab0 = dave), the concat buffer [M][2 cC] (CTXF: written; CTXB: read, = dcat) and fv [M][cC] (CTXF)
+  const float* ctab0 = nullptr;
+  const float* ctab1 = nullptr;
+  bf16_t* cat = nullptr;
+  const bf16_t* fvp = nullptr;
+  int cC = 0;
 };
 
 // pixel m of row r of pixel tile pt; EPI_POOLFWD tiles are 2 rows x TP/2 columns, rows interleaved per
@@ -502,6 +511,265 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
   }
   if constexpr (BPART) {
     if (a.bpart != nullptr) store_bias_partials(bs, a.bpart + (size_t)(pt * WP + wp) * a.Cout + chb, fr);
+  }
+}
+
+// ===========================================================================
+// Linearised context module (model/CANNet.py:42-87).
+// Per scale S, z_S = conv{S}_2(s_S - fv) with s_S = up(u_S) the bilinear
+// (align_corners) upsample of the S x S cells u_S = conv{S}_1(ave_S).  Both
+// the 1x1 conv and the upsample are linear per channel, so
+//     z_S = up(t_S) - G_S,   t_S = W2_S u_S (S x S cells),  G_S = W2_S fv,
+// and the four conv{S}_2 GEMMs over the 4 x [P x 512] expanded maps c_S
+// become ONE GEMM over fv itself: G = fv . W2cat^T with the 2048 columns
+// interleaved col' = 4c + si (W2cat[4c + si] = W2_S[c]), so every lane of the
+// MFMA D layout holds the four scales of 4 consecutive channels of one pixel.
+// EPI_CTXF (forward) then computes in registers
+//     w_S = sigmoid(up(t_S) - G_S),  fi = sum_S w_S up(u_S) / (sum_S w_S + 1e-12)
+// and writes w (a.y [M][4C], what the backward needs), fi and the fv copy into
+// the concat buffer (a.cat [M][2C]): c_S, the sigmoid maps and the separate
+// expand / fuse passes of the direct form (4 x 2 x 100 MB per 8 x 768 x 1024
+// batch) are never materialised.
+// EPI_CTXB (backward data gradient): x = dG = -dz [M][4C] (context.hip:
+// ctx_bwd_lin), W = W2cat^T [C][4C]; the epilogue adds the concat's direct
+// gradient dcat[:, :C], the adaptive-pool adjoint of dave and applies the
+// ReLU mask of fv (a.mask) -> dfv.
+// The up-sampling / pooling tables are separable: the block stages, for each
+// image row its 256 pixels touch (<= 5 rows: W >= 64, checked on the host),
+// the y-interpolated (CTXF) or y-pooled (CTXB) values of the 12 column bins
+// of the four scales (bins 0 | 1-2 | 3-5 | 6-11) in LDS after the main loop;
+// per pixel only the x weights remain.
+// ===========================================================================
+__device__ __forceinline__ void ctx_scale_of_bin(int bin, int& S, int& j, int& off) {
+  const int si = (bin >= 6) ? 3 : (bin >= 3) ? 2 : (bin >= 1) ? 1 : 0;
+  S = (si == 0) ? 1 : (si == 1) ? 2 : (si == 2) ? 3 : 6;
+  const int bo = (si == 0) ? 0 : (si == 1) ? 1 : (si == 2) ? 3 : 6;
+  off = (si == 0) ? 0 : (si == 1) ? 1 : (si == 2) ? 5 : 14;
+  j = bin - bo;
+}
+// bilinear taps (align_corners=True) of position x over length L at scale S
+__device__ __forceinline__ void ctx_bil(int S, int x, int L, int& x0, int& x1, float& lam) {
+  const float sc = (L > 1) ? (float)(S - 1) / (float)(L - 1) : 0.f;
+  const float src = sc * (float)x;
+  x0 = (int)src;
+  x1 = x0 + ((x0 < S - 1) ? 1 : 0);
+  lam = src - (float)x0;
+}
+// adaptive-pool bin [st, en) of index i at scale S over L (ATen: floor / ceil, overlapping when L % S != 0)
+__device__ __forceinline__ void ctx_pool_bin(int i, int S, int L, int& st, int& en) {
+  st = (i * L) / S;
+  en = ((i + 1) * L + S - 1) / S;
+}
+
+// CTXF table: tab[((lr * 2 + tensor) * 12 + bin) * 64 + cl], tensor 0 = t, 1 = u, cl = channel in the
+// 64-channel tile, value = y-bilinear mix of the two cell rows of row rlo + lr.  Built in the kernel's prologue into
+// LDS beside the staging ring (<= 5 rows = 30 KB): every global load of the (<= 4) items of a thread is issued before
+// the first LDS write, and the writes are made visible by the main loop's first barrier.
+constexpr int kCtxfTabBytes = 5 * 2 * 12 * 64 * 4;
+__device__ __forceinline__ void ctxf_build_tab(const ConvArgs2& a, float* tab, int ct, int rlo, int nr) {
+  const int C = a.cC;
+  const int items = nr * 2 * 12 * 16;
+  float4 p0[4], p1[4];
+  float lyv[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int it = threadIdx.x + q * blockDim.x;
+    p0[q] = p1[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    lyv[q] = 0.f;
+    if (it < items) {
+      const int c4 = it & 15, rest = it >> 4, bin = rest % 12, lt = rest / 12, tsr = lt & 1, lr = lt >> 1;
+      const int r = rlo + lr;
+      const int n = (int)fdiv((uint32_t)r, a.fdH), y = r - n * a.H;
+      int S, j, off;
+      ctx_scale_of_bin(bin, S, j, off);
+      int y0, y1;
+      ctx_bil(S, y, a.H, y0, y1, lyv[q]);
+      const float* T = (tsr ? a.ctab1 : a.ctab0) + ((size_t)n * 50 + off) * C + ct * 64 + c4 * 4;
+      p0[q] = *reinterpret_cast<const float4*>(T + (size_t)(y0 * S + j) * C);
+      p1[q] = *reinterpret_cast<const float4*>(T + (size_t)(y1 * S + j) * C);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int it = threadIdx.x + q * blockDim.x;
+    if (it < items) {
+      const int c4 = it & 15, rest = it >> 4, bin = rest % 12, lt = rest / 12;
+      const float ly = lyv[q], l0 = 1.f - ly;
+      *reinterpret_cast<float4*>(tab + ((size_t)lt * 12 + bin) * 64 + c4 * 4) =
+          make_float4(l0 * p0[q].x + ly * p1[q].x, l0 * p0[q].y + ly * p1[q].y, l0 * p0[q].z + ly * p1[q].z,
+                      l0 * p0[q].w + ly * p1[q].w);
+    }
+  }
+}
+
+// CTXB table: tab[(lr * 12 + bin) * 256 + cl] = sum over the pool cells (i, j(bin)) whose row bin contains row
+// rlo + lr of dave[cell][c] / cell area (cl = channel in the 256-channel tile)
+__device__ __forceinline__ void ctxb_build_tab(const ConvArgs2& a, float* tab, int ct, int rlo, int nr) {
+  const int C = a.cC;
+  for (int it = threadIdx.x; it < nr * 12 * 64; it += blockDim.x) {
+    const int c4 = it & 63, rest = it >> 6, bin = rest % 12, lr = rest / 12;
+    const int r = rlo + lr;
+    const int n = (int)fdiv((uint32_t)r, a.fdH), y = r - n * a.H;
+    int S, j, off;
+    ctx_scale_of_bin(bin, S, j, off);
+    int xs, xe;
+    ctx_pool_bin(j, S, a.W, xs, xe);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = 0; i < S; ++i) {
+      int ys, ye;
+      ctx_pool_bin(i, S, a.H, ys, ye);
+      if (y < ys || y >= ye) continue;
+      const float inv = 1.f / (float)((ye - ys) * (xe - xs));
+      const float4 d = *reinterpret_cast<const float4*>(a.ctab0 + ((size_t)n * 50 + off + i * S + j) * C + ct * 256 +
+                                                        c4 * 4);
+      acc.x += d.x * inv; acc.y += d.y * inv; acc.z += d.z * inv; acc.w += d.w * inv;
+    }
+    *reinterpret_cast<float4*>(tab + ((size_t)lr * 12 + bin) * 256 + c4 * 4) = acc;
+  }
+}
+
+template <int DT, int WC, int WP, int PW>
+__device__ __forceinline__ void ctxf_epilogue(const ConvArgs2& a, f32x4 (&acc)[4][4 * PW], const float* tab, int ct,
+                                              int pt, int rlo, int wc, int wp, int fr, int fq) {
+  constexpr int TP = 64 * PW * WP, NF = 4 * PW;
+  const int C = a.cC;
+  const int cl0 = wc * 16 + fq * 4;                 // this lane's first channel in the 64-channel tile
+  const int c0 = ct * 64 + cl0;
+  const int chb = ct * 256 + wc * 64 + fq * 16;     // this lane's first GEMM column (= 4 * c0)
+  uint2 fvw[NF];
+#pragma unroll
+  for (int i = 0; i < NF; ++i) {
+    const int m = pt * TP + wp * 64 * PW + i * 16 + fr;
+    fvw[i] = make_uint2(0u, 0u);
+    if (m < a.M) fvw[i] = *reinterpret_cast<const uint2*>(a.fvp + (size_t)m * C + c0);
+  }
+#pragma unroll
+  for (int i = 0; i < NF; ++i) {
+    const int m = pt * TP + wp * 64 * PW + i * 16 + fr;
+    if (m >= a.M) continue;
+    const int r = (int)fdiv((uint32_t)m, a.fdW), x = m - r * a.W;
+    const float* tr = tab + (size_t)(r - rlo) * 2 * 12 * 64 + cl0;
+    // T[si][j], U[si][j]: up(t), up(u) of the 4 scales at this pixel, channels c0 + j
+    float T[4][4], U[4][4];
+    {
+      const float4 t = *reinterpret_cast<const float4*>(tr);
+      const float4 u = *reinterpret_cast<const float4*>(tr + 12 * 64);
+      T[0][0] = t.x; T[0][1] = t.y; T[0][2] = t.z; T[0][3] = t.w;
+      U[0][0] = u.x; U[0][1] = u.y; U[0][2] = u.z; U[0][3] = u.w;
+    }
+#pragma unroll
+    for (int si = 1; si < 4; ++si) {
+      const int S = (si == 1) ? 2 : (si == 2) ? 3 : 6, bo = (si == 1) ? 1 : (si == 2) ? 3 : 6;
+      int x0, x1;
+      float lx;
+      ctx_bil(S, x, a.W, x0, x1, lx);
+      const float l0 = 1.f - lx;
+      const float4 t0 = *reinterpret_cast<const float4*>(tr + (bo + x0) * 64);
+      const float4 t1 = *reinterpret_cast<const float4*>(tr + (bo + x1) * 64);
+      const float4 u0 = *reinterpret_cast<const float4*>(tr + (12 + bo + x0) * 64);
+      const float4 u1 = *reinterpret_cast<const float4*>(tr + (12 + bo + x1) * 64);
+      T[si][0] = l0 * t0.x + lx * t1.x; T[si][1] = l0 * t0.y + lx * t1.y;
+      T[si][2] = l0 * t0.z + lx * t1.z; T[si][3] = l0 * t0.w + lx * t1.w;
+      U[si][0] = l0 * u0.x + lx * u1.x; U[si][1] = l0 * u0.y + lx * u1.y;
+      U[si][2] = l0 * u0.z + lx * u1.z; U[si][3] = l0 * u0.w + lx * u1.w;
+    }
+    float wv[16], fi[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float num = 0.f, den = 0.f;
+#pragma unroll
+      for (int si = 0; si < 4; ++si) {
+        const float z = T[si][j] - acc[j][i][si];
+        const float w = __builtin_amdgcn_rcpf(1.f + __expf(-z));   // v_rcp_f32 (1 ulp): the output is 16-bit
+        wv[j * 4 + si] = w;
+        num += w * U[si][j];
+        den += w;
+      }
+      fi[j] = num * __builtin_amdgcn_rcpf(den + 1e-12f);
+    }
+    bf16_t* yo = a.y + (size_t)m * a.Cout + chb;
+    *reinterpret_cast<uint4*>(yo) = pack8h<DT>(wv);
+    *reinterpret_cast<uint4*>(yo + 8) = pack8h<DT>(wv + 8);
+    bf16_t* co = a.cat + (size_t)m * 2 * C + c0;
+    *reinterpret_cast<uint2*>(co) = fvw[i];
+    *reinterpret_cast<uint2*>(co + C) = make_uint2(pack2<DT>(fi[0], fi[1]), pack2<DT>(fi[2], fi[3]));
+  }
+}
+
+// adaptive-pool column bins of scale S containing x: jA always, jB (or -1) when two bins overlap at x
+__device__ __forceinline__ void ctx_pool_cols(int S, int x, int L, int& jA, int& jB) {
+  jA = (x * S) / L;
+  jB = -1;
+  if (jA > 0 && ((jA * L + S - 1) / S) > x) jB = jA - 1;                 // end of bin jA - 1 reaches past x
+  else if (jA + 1 < S && ((jA + 1) * L) / S <= x) jB = jA + 1;           // bin jA + 1 starts at or before x
+}
+
+template <int DT, int WC, int WP, int PW>
+__device__ __forceinline__ void ctxb_epilogue(const ConvArgs2& a, f32x4 (&acc)[4][4 * PW], const float* tab, int ct,
+                                              int pt, int rlo, int wc, int wp, int fr, int fq) {
+  constexpr int TP = 64 * PW * WP, NF = 4 * PW, HALF = 2;
+  const int C = a.cC;
+  const int cl = wc * 64 + fq * 16;                 // this lane's first channel in the 256-channel tile
+  const int chb = ct * 256 + cl;
+  // groups of 2 pixel fragments: the dcat / mask loads of a group are issued before its first store (more in
+  // flight spills: the 128 accumulators are live throughout)
+#pragma unroll
+  for (int h = 0; h < NF / HALF; ++h) {
+    uint4 g0[HALF], g1[HALF], k0[HALF], k1[HALF];
+#pragma unroll
+    for (int ii = 0; ii < HALF; ++ii) {
+      const int m = pt * TP + wp * 64 * PW + (h * HALF + ii) * 16 + fr;
+      g0[ii] = g1[ii] = k0[ii] = k1[ii] = make_uint4(0u, 0u, 0u, 0u);
+      if (m < a.M) {
+        const bf16_t* gp = a.cat + (size_t)m * 2 * C + chb;
+        const bf16_t* kp = a.mask + (size_t)m * C + chb;
+        g0[ii] = *reinterpret_cast<const uint4*>(gp);
+        g1[ii] = *reinterpret_cast<const uint4*>(gp + 8);
+        k0[ii] = *reinterpret_cast<const uint4*>(kp);
+        k1[ii] = *reinterpret_cast<const uint4*>(kp + 8);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);           // vmcnt(0): only stores are outstanding below
+#pragma unroll
+    for (int ii = 0; ii < HALF; ++ii) {
+      const int i = h * HALF + ii;
+      const int m = pt * TP + wp * 64 * PW + i * 16 + fr;
+      if (m >= a.M) continue;
+      const int r = (int)fdiv((uint32_t)m, a.fdW), x = m - r * a.W;
+      const float* tr = tab + (size_t)(r - rlo) * 12 * 256 + cl;
+      float v[16];
+      unpack8h<DT>(g0[ii], v);
+      unpack8h<DT>(g1[ii], v + 8);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) v[j * 4 + rr] += acc[j][i][rr];
+      auto add_bin = [&](int bin, float wgt) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 t = *reinterpret_cast<const float4*>(tr + bin * 256 + q * 4);
+          v[q * 4 + 0] += wgt * t.x; v[q * 4 + 1] += wgt * t.y; v[q * 4 + 2] += wgt * t.z; v[q * 4 + 3] += wgt * t.w;
+        }
+      };
+      add_bin(0, 1.f);
+#pragma unroll 1
+      for (int si = 1; si < 4; ++si) {          // not unrolled: the hoisted table reads of 7 bins spill
+        const int S = (si == 1) ? 2 : (si == 2) ? 3 : 6, bo = (si == 1) ? 1 : (si == 2) ? 3 : 6;
+        int jA, jB;
+        ctx_pool_cols(S, x, a.W, jA, jB);
+        add_bin(bo + jA, 1.f);
+        add_bin(bo + (jB >= 0 ? jB : jA), jB >= 0 ? 1.f : 0.f);
+      }
+      const unsigned mw[8] = {k0[ii].x, k0[ii].y, k0[ii].z, k0[ii].w, k1[ii].x, k1[ii].y, k1[ii].z, k1[ii].w};
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const unsigned short bits = (unsigned short)(mw[c >> 1] >> ((c & 1) * 16));
+        v[c] = pos_bits(bits) ? v[c] : 0.f;
+      }
+      bf16_t* yo = a.y + (size_t)m * a.Cout + chb;
+      *reinterpret_cast<uint4*>(yo) = pack8h<DT>(v);
+      *reinterpret_cast<uint4*>(yo + 8) = pack8h<DT>(v + 8);
+    }
   }
 }
 
@@ -778,6 +1046,11 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
 
   frag8_t a0[4], b0[4 * PW], a1[4], b1[4 * PW];
   issue(0);
+  if constexpr (EPI == EPI_CTXF) {
+    // the up-sampling row tables, beside the staging ring (visible after the first barrier below)
+    const int rlo = (pt * TP) / a.W, rhi = (min(a.M, (pt + 1) * TP) - 1) / a.W;
+    ctxf_build_tab(a, reinterpret_cast<float*>(smem + 2 * STAGE), ct, rlo, rhi - rlo + 1);
+  }
   if (nk > 1) {
     issue(1);
     asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" :: "n"(GA + GB) : "memory");
@@ -832,13 +1105,31 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
   read((nk - 1) & 1, 1, a1, b1);
   mma(a0, b0, 0, 4 * PW);
   mma(a1, b1, 0, 4 * PW);
-  glds_epilogue<DT, WC, WP, PW, EPI>(a, acc, ct, pt, wc, wp, fr, fq);
+  if constexpr (EPI == EPI_CTXF || EPI == EPI_CTXB) {
+    static_assert(WC == 4 && WP == 2 && PW == 2, "context epilogues: 256 x 256 tiles");
+    // the staging LDS is free once every wave's last fragment reads are done: it holds the tile's row tables
+    const int rlo = (pt * TP) / a.W;
+    const int rhi = (min(a.M, (pt + 1) * TP) - 1) / a.W;
+    if constexpr (EPI == EPI_CTXF) {
+      ctxf_epilogue<DT, WC, WP, PW>(a, acc, reinterpret_cast<const float*>(smem + 2 * STAGE), ct, pt, rlo, wc, wp,
+                                    fr, fq);
+    } else {
+      float* tab = reinterpret_cast<float*>(smem);
+      __syncthreads();
+      ctxb_build_tab(a, tab, ct, rlo, rhi - rlo + 1);
+      __syncthreads();
+      ctxb_epilogue<DT, WC, WP, PW>(a, acc, tab, ct, pt, rlo, wc, wp, fr, fq);
+    }
+    return;
+  } else {
+    glds_epilogue<DT, WC, WP, PW, EPI>(a, acc, ct, pt, wc, wp, fr, fq);
+  }
 }
 
 template <int DT, int WC, int WP, int PW, int EPI>
 static int launch_glds2(const ConvArgs2& a, hipStream_t s, int nb = 1) {
   constexpr int TC = 64 * WC, TP = 64 * PW * WP;
-  const size_t lds = 2 * (size_t)(TC + TP) * 128;
+  const size_t lds = 2 * (size_t)(TC + TP) * 128 + (EPI == EPI_CTXF ? kCtxfTabBytes : 0);
   auto kfn = conv_glds2_kernel<DT, WC, WP, PW, EPI>;
   static bool attr = false;
   if (!attr) {
@@ -1815,6 +2106,30 @@ static int conv_igemm_batched_impl(const void* x, const void* w, const float* bi
   return -6;
 }
 
+// Linearised context module GEMMs (see "Linearised context module").  fwd = 1: x = fv [M][C], w = W2cat
+// [4C][C] -> y = w maps [M][4C], cat [M][2C] (fv | fi); tab0 = t, tab1 = u.  fwd = 0: x = dG [M][4C],
+// w = W2cat^T [C][4C], mask = fv, cat = dcat (read) -> y = dfv [M][C]; tab0 = dave.
+template <int DT>
+static int conv_ctx_impl(int fwd, const void* x, const void* w, const float* tab0, const float* tab1,
+                         const void* fv, void* cat, void* y, int N, int H, int W, int C, hipStream_t s) {
+  if (C % 256 || W < 64 || H < 1) return -2;       // 256 x 256 tiles; <= 5 image rows per 256-pixel tile
+  ConvArgs2 b;
+  b.x = (const bf16_t*)x; b.w = (const bf16_t*)w; b.bias = nullptr; b.y = (bf16_t*)y;
+  b.zero = conv_zero_page();
+  if (!b.zero) return -10;
+  b.H = H; b.W = W; b.ksize = 1; b.dil = 1; b.M = N * H * W;
+  b.Cin = fwd ? C : 4 * C;
+  b.Cout = fwd ? 4 * C : C;
+  b.fdW = make_fastdiv((uint32_t)W); b.fdH = make_fastdiv((uint32_t)H);
+  b.ctab0 = tab0; b.ctab1 = tab1; b.cat = (bf16_t*)cat; b.cC = C;
+  if (fwd) {
+    b.mask = nullptr; b.fvp = (const bf16_t*)fv;
+    return launch_glds2<DT, 4, 2, 2, EPI_CTXF>(b, s);
+  }
+  b.mask = (const bf16_t*)fv;
+  return launch_glds2<DT, 4, 2, 2, EPI_CTXB>(b, s);
+}
+
 // 3x3 / 1x1 conv + bias + ReLU with the 2x2/s2 max-pool fused into the epilogue: yp = pooled output,
 // codes = its max-pool codes (what the backward needs), y = the full-resolution output (optional: nullptr
 // skips its 2-byte-per-element store).  LDS-DMA v2 kernels and conv1_2's halo kernel.
@@ -1910,6 +2225,11 @@ extern "C" int can_conv_igemm_batched(const void* x, const void* w, const float*
                                       int dil, int epi, int tile_cfg, int dt, void* stream) {
   CAN_DT_DISPATCH(dt, can::conv_igemm_batched_impl<DT>(x, w, bias, y, nb, xbs, wbs, ybs, N, H, W, Cin, Cout, ksize, dil,
                                                       epi, tile_cfg, (hipStream_t)stream));
+}
+
+extern "C" int can_conv_ctx(int fwd, const void* x, const void* w, const float* tab0, const float* tab1, const void* fv,
+                            void* cat, void* y, int N, int H, int W, int C, int dt, void* stream) {
+  CAN_DT_DISPATCH(dt, can::conv_ctx_impl<DT>(fwd, x, w, tab0, tab1, fv, cat, y, N, H, W, C, (hipStream_t)stream));
 }
 
 extern "C" int can_conv_pool_fwd(const void* x, const void* w, const float* bias, void* y, void* yp, void* codes,

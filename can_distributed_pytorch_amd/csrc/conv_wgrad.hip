@@ -1348,6 +1348,8 @@ extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, in
   if (first) cfg = 0;
   else if (halo_ok && getenv("CANNET_NO_HALO") == nullptr && M >= 262144) cfg = 8;
   else if (Cout % 256 == 0 && K >= 2048) cfg = (K % 256 == 0 && getenv("CANNET_WGRAD_V1") == nullptr) ? 9 : 7;
+  else if (Cout % 256 == 0 && ksize == 1 && K % 256 == 0 && K >= 512 && getenv("CANNET_WGRAD_V1") == nullptr)
+    cfg = 9;   // 1x1 with many output rows (the linearised context module's dW2cat: 2048 x 512)
   else if (Cout % 256 == 0 && K >= 1024)
     cfg = (Cin % 128 == 0 && getenv("CANNET_WGRAD_V1") == nullptr && getenv("CANNET_WGRAD_NO_HALF") == nullptr) ? 10 : 2;
   else if (Cout == 128 && Cin % 256 == 0 && K >= 2048 && getenv("CANNET_WGRAD_V1") == nullptr &&

@@ -386,7 +386,8 @@ __global__ void __launch_bounds__(256) pack_conv_kernel(const float* __restrict_
 }
 
 // All layers' packs in one launch: blockIdx.y = layer, descriptor rows
-// {w, fwd, dgr, Co, Ci, taps, first, 0} (int64).  blockIdx.x = a 32(co) x
+// {w, fwd, dgr, Co, Ci, taps, first, mode} (int64; mode 1 + si: the scale-si rows of the interleaved context
+// packs, see below).  blockIdx.x = a 32(co) x
 // 32(ci) x taps tile transposed through LDS, so the fp32 reads (ci, tap
 // contiguous per co), the fwd-pack writes (ci contiguous per co, tap) and the
 // dgrad-pack writes (co contiguous per ci, tap) are all coalesced.
@@ -426,6 +427,20 @@ __global__ void __launch_bounds__(256) pack_multi_kernel(const long long* __rest
     for (int i = threadIdx.x; i < cos_ * row; i += 256) {
       const int c = i / row, r = i - c * row, ci = r / taps, tap = r - ci * taps;
       fwd[(size_t)(co0 + c) * 64 + tap * 4 + ci0 + ci] = t[c][r];
+    }
+    return;
+  }
+  if (d[7] > 0) {
+    // linearised context module (conv_igemm.hip): W2cat[4co + si][ci] = W2_S[co][ci] (fwd, rows interleaved over
+    // the four scales) and its transpose W2cat^T[ci][4co + si] (dgr); 1x1 only, si = d[7] - 1
+    const int si = (int)d[7] - 1;
+    for (int i = threadIdx.x; i < cos_ * cis; i += 256) {
+      const int ci = i % cis, c = i / cis;
+      fwd[((size_t)4 * (co0 + c) + si) * Ci + ci0 + ci] = t[c][ci];
+    }
+    for (int i = threadIdx.x; i < cis * cos_; i += 256) {
+      const int c = i % cos_, ci = i / cos_;
+      dgr[(size_t)(ci0 + ci) * 4 * Co + 4 * (co0 + c) + si] = t[c][ci];
     }
     return;
   }

@@ -533,3 +533,73 @@ def conv_dgrad_w1g(dy: torch.Tensor, wpack: torch.Tensor, mask: torch.Tensor, im
     C.wgrad_reduce_first(slabs.data_ptr(), bslabs.data_ptr(), dw1.data_ptr(), db1.data_ptr(), s, float(beta),
                          float(scale), dscale.data_ptr() if dscale is not None else 0, st)
     return out
+
+
+# ---------------------------------------------------------------------------------------------------------------------
+# Linearised context module (csrc/conv_igemm.hip "Linearised context module", csrc/context.hip ctx_bwd_lin)
+# ---------------------------------------------------------------------------------------------------------------------
+def ctx_linear_ok(fv: torch.Tensor) -> bool:
+    """The one-GEMM context module needs 256-channel tiles and a 256-pixel tile spanning <= 5 image rows (W >= 64)."""
+    return fv.dim() == 4 and fv.shape[-1] % 256 == 0 and fv.shape[2] >= 64
+
+
+def _check_cells(t: torch.Tensor, n: int, c: int, name: str):
+    if t.dtype != torch.float32 or not t.is_contiguous() or tuple(t.shape) != (n, 50, c) or not t.is_cuda:
+        raise ValueError(f"{name} must be a contiguous fp32 GPU tensor [{n}, 50, {c}]")
+
+
+def conv_ctx_fwd(fv: torch.Tensor, wcat: torch.Tensor, t: torch.Tensor, u: torch.Tensor):
+    """fv [N,h,w,C] -> (w maps [N,h,w,4C] (sigmoid of the four scales, columns 4c + si), cat [N,h,w,2C] = fv | fi).
+    wcat: [4C, C] interleaved conv{S}_2 pack; t = W2 u, u = W1 ave: fp32 cell tables [N, 50, C]."""
+    C = _ext.require()
+    _check_act(fv, "fv")
+    n, h, w, c = fv.shape
+    if not ctx_linear_ok(fv):
+        raise ValueError("conv_ctx_fwd needs C % 256 == 0 and w >= 64")
+    if wcat.dtype != fv.dtype or not wcat.is_contiguous() or tuple(wcat.shape) != (4 * c, c):
+        raise ValueError(f"wcat must be a contiguous {fv.dtype} [{4 * c}, {c}] pack")
+    _check_cells(t, n, c, "t")
+    _check_cells(u, n, c, "u")
+    wts = torch.empty(n, h, w, 4 * c, dtype=fv.dtype, device=fv.device)
+    cat = torch.empty(n, h, w, 2 * c, dtype=fv.dtype, device=fv.device)
+    C.conv_ctx(1, fv.data_ptr(), wcat.data_ptr(), t.data_ptr(), u.data_ptr(), fv.data_ptr(), cat.data_ptr(),
+               wts.data_ptr(), n, h, w, c, dt_code(fv.dtype), _ext.stream_ptr(fv.device))
+    return wts, cat
+
+
+def ctx_bwd_lin(dcat: torch.Tensor, wts: torch.Tensor, u: torch.Tensor):
+    """(dG [N,h,w,4C] = -dz, row partials [2, N, h, 12, C] of up^T(dz) and up^T(ds)) from dcat [N,h,w,2C]."""
+    C = _ext.require()
+    _check_act(wts, "wts")
+    n, h, w, c4 = wts.shape
+    c = c4 // 4
+    _check_act(dcat, "dcat", dtype=wts.dtype)
+    if tuple(dcat.shape) != (n, h, w, 2 * c) or c % 128:
+        raise ValueError("dcat / wts shapes")
+    _check_cells(u, n, c, "u")
+    dg = torch.empty_like(wts)
+    rowacc = torch.empty(2, n, h, 12, c, dtype=torch.float32, device=wts.device)
+    C.ctx_bwd_lin(dcat.data_ptr(), wts.data_ptr(), u.data_ptr(), dg.data_ptr(), rowacc.data_ptr(), n, h, w, c,
+                  dt_code(wts.dtype), _ext.stream_ptr(wts.device))
+    return dg, rowacc
+
+
+def conv_ctx_bwd(dg: torch.Tensor, wcat_dgr: torch.Tensor, dave: torch.Tensor, dcat: torch.Tensor,
+                 fv: torch.Tensor) -> torch.Tensor:
+    """dfv [N,h,w,C] = (dG . W2cat + dcat[..., :C] + pool^T(dave)) * (fv > 0)."""
+    C = _ext.require()
+    _check_act(fv, "fv")
+    n, h, w, c = fv.shape
+    if not ctx_linear_ok(fv):
+        raise ValueError("conv_ctx_bwd needs C % 256 == 0 and w >= 64")
+    _check_act(dg, "dg", 4 * c, dtype=fv.dtype)
+    _check_act(dcat, "dcat", 2 * c, dtype=fv.dtype)
+    if tuple(dg.shape[:3]) != (n, h, w) or tuple(dcat.shape[:3]) != (n, h, w):
+        raise ValueError("dg / dcat spatial shape")
+    if wcat_dgr.dtype != fv.dtype or not wcat_dgr.is_contiguous() or tuple(wcat_dgr.shape) != (c, 4 * c):
+        raise ValueError(f"wcat_dgr must be a contiguous {fv.dtype} [{c}, {4 * c}] pack")
+    _check_cells(dave, n, c, "dave")
+    dfv = torch.empty_like(fv)
+    C.conv_ctx(0, dg.data_ptr(), wcat_dgr.data_ptr(), dave.data_ptr(), 0, fv.data_ptr(), dcat.data_ptr(),
+               dfv.data_ptr(), n, h, w, c, dt_code(fv.dtype), _ext.stream_ptr(fv.device))
+    return dfv

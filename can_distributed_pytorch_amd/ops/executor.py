@@ -13,7 +13,8 @@ fp32 weights change.
 Forward (training) saves exactly what the backward needs: every conv input
 (NHWC bf16), the max-pool codes of the three pools (4-bit first-max one-hots:
 the full-resolution pre-pool activations are never stored), the context
-tables, c_S and w_S.
+cell tables and the sigmoid maps w_S (linearised context module: c_S is
+never formed).
 Backward (per layer, reverse order) = weight-gradient (split-pixel MFMA +
 deterministic slab reduction) + data-gradient (same MFMA kernel as forward,
 flipped weights, ReLU mask / maxpool-backward fused), and after each layer's
@@ -131,6 +132,10 @@ class CANNetExecutor:
         self.ctx2_dgr = torch.empty_like(self.ctx2_fwd)
         for i, sc in enumerate(CONTEXT_SCALES):
             self.packs[id(self.ctx2[sc].weight)] = (self.ctx2_fwd[i], self.ctx2_dgr[i])
+        # the linearised context module's interleaved packs: W2cat[4c + si] = W2_S[c] and its transpose
+        nsc = len(CONTEXT_SCALES)
+        self.ctx2cat_fwd = torch.empty(nsc * 512, 512, dtype=self.act, device=device)
+        self.ctx2cat_dgr = torch.empty(512, nsc * 512, dtype=self.act, device=device)
 
     def refresh_packs(self, force: bool = False):
         """Re-pack the 16-bit weight copies from the fp32 masters (one launch for all layers)."""
@@ -150,13 +155,16 @@ class CANNetExecutor:
             for sc in CONTEXT_SCALES:
                 fwd, dgr = self.packs[id(self.ctx2[sc].weight)]
                 rows.append([self.ctx2[sc].weight.data_ptr(), fwd.data_ptr(), dgr.data_ptr(), 512, 512, 1, 0, 0])
+            for si, sc in enumerate(CONTEXT_SCALES):
+                rows.append([self.ctx2[sc].weight.data_ptr(), self.ctx2cat_fwd.data_ptr(),
+                             self.ctx2cat_dgr.data_ptr(), 512, 512, 1, 0, 1 + si])
             self._pack_desc = torch.tensor(rows, dtype=torch.int64, device=dev)
             self._pack_desc_ptrs = tuple(r[0] for r in rows)
             self._pack_tiles = max(((r[3] + 31) // 32) * ((r[4] + 31) // 32) for r in rows)
         # one launch for every layer (descriptor rows hold the fp32 master pointers,
         # which the flat arena keeps fixed; rebuilt if a weight tensor moved)
         cur = tuple(s.module.weight.data_ptr() for s in self.front + self.back) + \
-            tuple(self.ctx2[sc].weight.data_ptr() for sc in CONTEXT_SCALES)
+            tuple(self.ctx2[sc].weight.data_ptr() for sc in CONTEXT_SCALES) * 2
         if cur != self._pack_desc_ptrs:
             self._pack_desc = None
             return self.refresh_packs(force=True)
@@ -184,6 +192,7 @@ class CANNetExecutor:
         for s in self.back:
             need = max(need, self.ws.plan(n * hh * ww, s.cin, s.cout, 3, False, s.dil)[3])
         need = max(need, self.ws.plan(n * hh * ww, 512, 512, 1, False)[3])
+        need = max(need, self.ws.plan(n * hh * ww, 512, 4 * 512, 1, False)[3])    # linearised context dW2cat
         need = max(need, max(C.wgrad_1x1_batched_plan(n * hh * ww, 4, 512, 512, ncu=c)[2] for c in (128, 192, 224, 256)))
         need = max(need, C.conv_wgrad_f1_need(n * h * w))
         self.ws.reserve(need)
@@ -308,7 +317,15 @@ class CANNetExecutor:
             sv.update(front_in=acts, pre_pool=pre_pool, fv=fv, ctx=ctx_saved, back_in=back_in, b6=x, f1=f1)
         return x, sv
 
+    @staticmethod
+    def _ctx_linear(fv) -> bool:
+        """The context module as one GEMM each way (conv_igemm.hip "Linearised context module"); CANNET_CTX_LINEAR=0
+        or a map narrower than 64 columns: the direct per-scale form (expand -> 4 sigmoid GEMMs -> fuse)."""
+        return os.environ.get("CANNET_CTX_LINEAR", "1") != "0" and C.ctx_linear_ok(fv)
+
     def _context_fwd(self, fv, save):
+        if self._ctx_linear(fv):
+            return self._context_fwd_linear(fv, save)
         n, h, w, c = fv.shape
         st = self._stream()
         rowacc = torch.empty(n, h, 12, c, dtype=torch.float32, device=fv.device)
@@ -330,6 +347,27 @@ class CANNetExecutor:
         self.C.ctx_fuse(fv.data_ptr(), wts.data_ptr(), table.data_ptr(), cat.data_ptr(), n, h, w, c, self.dt, st)
         saved = dict(ave=ave, table=table, cs=cs, wts=wts, rowacc=rowacc) if save else None
         return cat, saved
+
+    def _context_fwd_linear(self, fv, save):
+        n, h, w, c = fv.shape
+        st = self._stream()
+        rowacc = torch.empty(n, h, 12, c, dtype=torch.float32, device=fv.device)
+        ave = torch.empty(n, 50, c, dtype=torch.float32, device=fv.device)
+        self.C.ctx_reduce(0, fv.data_ptr(), 0, 0, rowacc.data_ptr(), ave.data_ptr(), n, h, w, c, self.dt, st)
+        u = torch.empty_like(ave)            # conv{S}_1 on the pooled cells
+        self.C.ctx_gemm(0, ave.data_ptr(), 0, self._ctx1_ptrs(), u.data_ptr(), [], n, c, 0.0, 1.0, 0, st)
+        t = torch.empty_like(ave)            # conv{S}_2 on the same cells (its upsample is z's first term)
+        self.C.ctx_gemm(0, u.data_ptr(), 0, self._ctx2_ptrs(), t.data_ptr(), [], n, c, 0.0, 1.0, 0, st)
+        wts, cat = C.conv_ctx_fwd(fv, self.ctx2cat_fwd, t, u)
+        saved = dict(linear=True, ave=ave, u=u, wts=wts) if save else None
+        return cat, saved
+
+    def _ctx2_ptrs(self):
+        ws = [self.ctx2[sc].weight for sc in CONTEXT_SCALES]
+        for w_ in ws:
+            if not (w_.is_contiguous() and w_.dtype == torch.float32):
+                raise ValueError("conv{S}_2 weights must be contiguous fp32")
+        return [w_.data_ptr() for w_ in ws]
 
     @staticmethod
     def _ctx_batched(h, w):
@@ -491,8 +529,55 @@ class CANNetExecutor:
             fn()
         hold.extend(keep)
 
+    def _context_bwd_linear(self, ctx, fv, dcat, grads, ws, beta, scale, ready, dscale=None, side=None, hold=None):
+        """Backward of the linearised context module (see _context_fwd_linear); returns d(F10 pre-activation)."""
+        st = self._stream()
+        n, h, w, c = fv.shape
+        hold = [] if hold is None else hold
+        dg, rowacc = C.ctx_bwd_lin(dcat, ctx["wts"], ctx["u"])        # dG = -dz, x-pass partials of up^T
+        dt = torch.empty(n, 50, c, dtype=torch.float32, device=fv.device)
+        du = torch.empty_like(dt)
+        self.C.ctx_cells(rowacc[0].data_ptr(), dt.data_ptr(), n, h, c, st)     # dt_S = up^T(dz_S)
+        self.C.ctx_cells(rowacc[1].data_ptr(), du.data_ptr(), n, h, c, st)     # du_S = up^T(ds_S)   (direct part)
+        u, ave = ctx["u"], ctx["ave"]
+        dw2 = [grads[self.ctx2_index[sc]] for sc in CONTEXT_SCALES]
+        for g in dw2:
+            if not (g.is_contiguous() and g.dtype == torch.float32):
+                raise ValueError("conv{S}_2 gradient buffers must be contiguous fp32")
+        if getattr(self, "_dw2cat", None) is None or self._dw2cat.device != fv.device:
+            self._dw2cat = torch.empty(4 * c, c, 1, 1, dtype=torch.float32, device=fv.device)
+        dw2cat = self._dw2cat
+        dsp = dscale.data_ptr() if dscale is not None else 0
+
+        def ctx2_wgrad():
+            # dW2_S = dG_S^T fv (one GEMM over the interleaved columns) + dt_S^T u_S (the t = W2 u term)
+            C.conv_wgrad(dg, fv, dw2cat, None, ksize=1, ws=ws, beta=0.0, scale=scale, dscale=dscale)
+            self.C.ctx_w2_scatter(dw2cat.data_ptr(), [g.data_ptr() for g in dw2], c, float(beta), self._stream())
+            self.C.ctx_gemm(2, dt.data_ptr(), u.data_ptr(), [], 0, [g.data_ptr() for g in dw2], n, c, 1.0,
+                            float(scale), dsp, self._stream())
+            ready([self.ctx2_index[sc] for sc in CONTEXT_SCALES])
+        self._on_side(side, ctx2_wgrad, hold, dg, fv, dt, u)
+        # du_S += W2_S^T dt_S, then dave_S = W1_S^T du_S (fp32 cell GEMMs)
+        self.C.ctx_gemm(1, dt.data_ptr(), 0, self._ctx2_ptrs(), du.data_ptr(), [], n, c, 1.0, 1.0, 0, st)
+
+        def ctx1_wgrad():
+            gws = [grads[self.ctx1_index[sc]] for sc in CONTEXT_SCALES]
+            for g in gws:
+                if not (g.is_contiguous() and g.dtype == torch.float32):
+                    raise ValueError("conv{S}_1 gradient buffers must be contiguous fp32")
+            self.C.ctx_gemm(2, du.data_ptr(), ave.data_ptr(), [], 0, [g.data_ptr() for g in gws], n, c, float(beta),
+                            float(scale), dsp, self._stream())
+            ready([self.ctx1_index[sc] for sc in CONTEXT_SCALES])
+        self._on_side(side, ctx1_wgrad, hold, du, ave)
+        dave = torch.empty_like(du)
+        self.C.ctx_gemm(1, du.data_ptr(), 0, self._ctx1_ptrs(), dave.data_ptr(), [], n, c, 0.0, 1.0, 0, st)
+        hold.append(rowacc)
+        return C.conv_ctx_bwd(dg, self.ctx2cat_dgr, dave, dcat, fv)
+
     def _context_bwd(self, ctx, fv, dcat, grads, ws, beta, scale, ready, dscale=None, side=None, hold=None):
         """Backward of the context module; returns d(F10 pre-activation) (ReLU mask of fv applied)."""
+        if ctx.get("linear"):
+            return self._context_bwd_linear(ctx, fv, dcat, grads, ws, beta, scale, ready, dscale, side, hold)
         st = self._stream()
         n, h, w, c = fv.shape
         dz = torch.empty(4, n, h, w, c, dtype=self.act, device=fv.device)
