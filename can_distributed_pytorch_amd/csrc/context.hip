@@ -21,6 +21,7 @@
 // fixed-order (deterministic, no atomics).  Adaptive-pool bins follow ATen:
 // start = floor(i*L/S), end = ceil((i+1)*L/S) (overlapping when L % S != 0).
 #include "common.h"
+#include <stdlib.h>
 
 namespace can {
 
@@ -763,6 +764,93 @@ __global__ void __launch_bounds__(256) ctx_gemm_kernel(CtxGemmArgs a) {
   }
 }
 
+// ctx_mm_kernel: the same three cell GEMMs on the fp32 matrix cores (v_mfma_f32_16x16x4_f32: f32 in, exact f32
+// FMA chain).  These GEMMs are latency-bound, not FLOP-bound (<= 0.3 GFLOP per launch): the 32 x 64-tile kernel
+// above ran ~1 wave per SIMD through 16 dependent K steps (34-47 us per launch).  Here a block of 8 waves owns one
+// 16 x 16 output tile of one scale and splits K 8 ways (each wave <= 16 MFMAs over 4-deep K chunks whose operands
+// are all loaded before the first MFMA); the 8 partial tiles are summed in LDS in a fixed order (deterministic).
+// The K order inside a 16-chunk is permuted (step s, lane group q -> k = 16c + 4q + s) identically for A and B, so
+// K-contiguous operands load as one float4 per lane per chunk.
+template <int MODE>
+__global__ void __launch_bounds__(512) ctx_mm_kernel(CtxGemmArgs a) {
+  __shared__ f32x4 red[8][64];
+  const int si = blockIdx.z;
+  const int S = (si == 0) ? 1 : (si == 1) ? 2 : (si == 2) ? 3 : 6;
+  const int off = (si == 0) ? 0 : (si == 1) ? 1 : (si == 2) ? 5 : 14;
+  const int k2 = S * S, R = a.N * k2, C = a.C;
+  const int M = (MODE == 2) ? C : R, K = (MODE == 2) ? R : C;
+  const int m0 = blockIdx.y * 16, n0 = blockIdx.x * 16;
+  if (m0 >= M) return;
+  const float* W = a.w[si];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, q = lane >> 4;
+  // this wave's K range, whole 16-chunks
+  const int nch = (K + 15) / 16;
+  const int cpw = (nch + 7) / 8;
+  const int c0 = wave * cpw, c1 = min(nch, c0 + cpw);
+  constexpr int MAXC = 4;                           // K <= 8 * 4 * 16 = 512 (C = 512; R <= 8 * 36 = 288)
+  float av[MAXC][4], bv[MAXC][4];
+#pragma unroll
+  for (int cc = 0; cc < MAXC; ++cc) {
+    const int ch = c0 + cc;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) { av[cc][s] = 0.f; bv[cc][s] = 0.f; }
+    if (ch >= c1) continue;
+    const int kb = ch * 16 + 4 * q;                 // this lane's 4 k values: kb .. kb + 3
+    const int m = m0 + i, n = n0 + i;
+    if (MODE == 0) {
+      // A(m,k) = cells[row(m)][k], B(k,n) = W[n][k]: both k-contiguous
+      if (m < M) {
+        const float4 v = *reinterpret_cast<const float4*>(a.x + (size_t)ctx_cell_row(m, k2, off) * C + kb);
+        av[cc][0] = v.x; av[cc][1] = v.y; av[cc][2] = v.z; av[cc][3] = v.w;
+      }
+      const float4 v = *reinterpret_cast<const float4*>(W + (size_t)n * C + kb);
+      bv[cc][0] = v.x; bv[cc][1] = v.y; bv[cc][2] = v.z; bv[cc][3] = v.w;
+    } else if (MODE == 1) {
+      // A(m,k) = cells[row(m)][k] (k-contiguous), B(k,n) = W[k][n]
+      if (m < M) {
+        const float4 v = *reinterpret_cast<const float4*>(a.x + (size_t)ctx_cell_row(m, k2, off) * C + kb);
+        av[cc][0] = v.x; av[cc][1] = v.y; av[cc][2] = v.z; av[cc][3] = v.w;
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) bv[cc][s] = W[(size_t)(kb + s) * C + n];
+    } else {
+      // A(m,k) = dA[row(k)][m], B(k,n) = ave[row(k)][n] (k = cell row r < R)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int k = kb + s;
+        if (k < K) {
+          const size_t rr = (size_t)ctx_cell_row(k, k2, off) * C;
+          av[cc][s] = a.x[rr + m];
+          bv[cc][s] = a.y[rr + n];
+        }
+      }
+    }
+  }
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int cc = 0; cc < MAXC; ++cc)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[cc][s], bv[cc][s], acc, 0, 0, 0);
+  red[wave][lane] = acc;
+  __syncthreads();
+  if (wave != 0) return;
+  f32x4 t = red[0][lane];
+#pragma unroll
+  for (int w8 = 1; w8 < 8; ++w8) t += red[w8][lane];
+  // D layout: column n0 + (lane & 15), rows m0 + 4 * (lane >> 4) + v
+  const int n = n0 + i;
+  const float sc = (MODE == 2) ? a.scale * ((a.dscale != nullptr) ? a.dscale[0] : 1.f) : 1.f;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int m = m0 + 4 * q + v;
+    if (m >= M) continue;
+    float* o = (MODE == 2) ? a.gw[si] + (size_t)m * C + n : a.out + (size_t)ctx_cell_row(m, k2, off) * C + n;
+    float val = t[v] * sc;
+    if (a.beta != 0.f) val += a.beta * *o;
+    *o = val;
+  }
+}
+
 static inline int gridn(size_t n, int cap = 8192) {
   size_t g = (n + 255) / 256;
   if (g > (size_t)cap) g = cap;
@@ -872,8 +960,17 @@ extern "C" int can_ctx_gemm(int mode, const float* x, const float* y, const floa
     a.gw[i] = gw ? gw[i] : nullptr;
   }
   const int M = (mode == 2) ? C : N * 36;
-  const dim3 grid(C / 64, (M + 31) / 32, 4);
   hipStream_t s = (hipStream_t)stream;
+  if (C <= 512 && N * 36 <= 512 && getenv("CANNET_CTX_GEMM_V1") == nullptr) {
+    // matrix-core form (K <= 512 on both sides): 16 x 16 tiles, K split over 8 waves
+    const dim3 grid(C / 16, (M + 15) / 16, 4);
+    if (mode == 0) hipLaunchKernelGGL(ctx_mm_kernel<0>, grid, dim3(512), 0, s, a);
+    else if (mode == 1) hipLaunchKernelGGL(ctx_mm_kernel<1>, grid, dim3(512), 0, s, a);
+    else if (mode == 2) hipLaunchKernelGGL(ctx_mm_kernel<2>, grid, dim3(512), 0, s, a);
+    else return -3;
+    return (int)hipGetLastError();
+  }
+  const dim3 grid(C / 64, (M + 31) / 32, 4);
   if (mode == 0) hipLaunchKernelGGL(ctx_gemm_kernel<0>, grid, dim3(256), 0, s, a);
   else if (mode == 1) hipLaunchKernelGGL(ctx_gemm_kernel<1>, grid, dim3(256), 0, s, a);
   else if (mode == 2) hipLaunchKernelGGL(ctx_gemm_kernel<2>, grid, dim3(256), 0, s, a);
