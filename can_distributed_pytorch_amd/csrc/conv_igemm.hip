@@ -332,6 +332,7 @@ struct ConvArgs2 {
   bf16_t* cat = nullptr;
   const bf16_t* fvp = nullptr;
   int cC = 0;
+  int ctx_prologue = 0;    // 1: the launch reserved LDS for the row tables beside the staging ring
 };
 
 // pixel m of row r of pixel tile pt; EPI_POOLFWD tiles are 2 rows x TP/2 columns, rows interleaved per
@@ -561,81 +562,93 @@ __device__ __forceinline__ void ctx_pool_bin(int i, int S, int L, int& st, int& 
   en = ((i + 1) * L + S - 1) / S;
 }
 
-// CTXF table: tab[((lr * 2 + tensor) * 12 + bin) * 64 + cl], tensor 0 = t, 1 = u, cl = channel in the
-// 64-channel tile, value = y-bilinear mix of the two cell rows of row rlo + lr.  Built in the kernel's prologue into
-// LDS beside the staging ring (<= 5 rows = 30 KB): every global load of the (<= 4) items of a thread is issued before
-// the first LDS write, and the writes are made visible by the main loop's first barrier.
-constexpr int kCtxfTabBytes = 5 * 2 * 12 * 64 * 4;
-__device__ __forceinline__ void ctxf_build_tab(const ConvArgs2& a, float* tab, int ct, int rlo, int nr) {
+// CTXF table: tab[((lr * 2 + tensor) * 12 + bin) * TCH + cl], tensor 0 = t, 1 = u, cl = channel in the
+// TCH-channel tile (TCH = TC / 4), value = y-bilinear mix of the two cell rows of row rlo + lr.
+// CTXB table: tab[(lr * 12 + bin) * TC + cl] = sum over the pool cells (i, j(bin)) whose row bin contains row
+// rlo + lr of dave[cell][c] / cell area (cl = channel in the TC-channel tile).
+// Both are built in the kernel's prologue into LDS beside the staging ring when they fit (every global load of a
+// thread's items is issued before its first LDS write; the main loop's first barrier makes them visible), else
+// (CTXB, 256 x 256 tiles) after the main loop in the freed staging LDS.
+__host__ __device__ constexpr int ctx_tab_row_bytes(int EPI_, int TC) {
+  return EPI_ == EPI_CTXF ? 2 * 12 * (TC / 4) * 4 : 12 * TC * 4;
+}
+__host__ __device__ constexpr int ctx_max_rows(int TP, int W) { return (TP - 1) / W + 2; }
+
+// adaptive-pool bins of scale S containing x (over L): jA always, jB (or -1) when two bins overlap at x
+__device__ __forceinline__ void ctx_pool_cols(int S, int x, int L, int& jA, int& jB) {
+  jA = (x * S) / L;
+  jB = -1;
+  if (jA > 0 && ((jA * L + S - 1) / S) > x) jB = jA - 1;                 // end of bin jA - 1 reaches past x
+  else if (jA + 1 < S && ((jA + 1) * L) / S <= x) jB = jA + 1;           // bin jA + 1 starts at or before x
+}
+
+template <int EPI, int TC, int NT, int Q>
+__device__ __forceinline__ void ctx_build_tab(const ConvArgs2& a, float* tab, int ct, int rlo, int nr) {
   const int C = a.cC;
-  const int items = nr * 2 * 12 * 16;
-  float4 p0[4], p1[4];
-  float lyv[4];
+  constexpr int TCH = (EPI == EPI_CTXF) ? TC / 4 : TC;      // table channels
+  constexpr int G4 = TCH / 4;                              // float4 groups per bin
+  constexpr int NB = (EPI == EPI_CTXF) ? 24 : 12;          // (tensor,) bin rows per image row
+  const int items = nr * NB * G4;
+  float4 p0[Q], p1[Q];
+  float l1[Q], l0[Q];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int it = threadIdx.x + q * blockDim.x;
+  for (int q = 0; q < Q; ++q) {
+    const int it = threadIdx.x + q * NT;
     p0[q] = p1[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-    lyv[q] = 0.f;
+    l0[q] = l1[q] = 0.f;
     if (it < items) {
-      const int c4 = it & 15, rest = it >> 4, bin = rest % 12, lt = rest / 12, tsr = lt & 1, lr = lt >> 1;
+      const int c4 = it % G4, rest = it / G4, bin = rest % 12, lt = rest / 12;
+      const int lr = (EPI == EPI_CTXF) ? (lt >> 1) : lt;
       const int r = rlo + lr;
       const int n = (int)fdiv((uint32_t)r, a.fdH), y = r - n * a.H;
       int S, j, off;
       ctx_scale_of_bin(bin, S, j, off);
-      int y0, y1;
-      ctx_bil(S, y, a.H, y0, y1, lyv[q]);
-      const float* T = (tsr ? a.ctab1 : a.ctab0) + ((size_t)n * 50 + off) * C + ct * 64 + c4 * 4;
-      p0[q] = *reinterpret_cast<const float4*>(T + (size_t)(y0 * S + j) * C);
-      p1[q] = *reinterpret_cast<const float4*>(T + (size_t)(y1 * S + j) * C);
+      if constexpr (EPI == EPI_CTXF) {
+        int y0, y1;
+        float ly;
+        ctx_bil(S, y, a.H, y0, y1, ly);
+        const float* T = ((lt & 1) ? a.ctab1 : a.ctab0) + ((size_t)n * 50 + off) * C + ct * TCH + c4 * 4;
+        p0[q] = *reinterpret_cast<const float4*>(T + (size_t)(y0 * S + j) * C);
+        p1[q] = *reinterpret_cast<const float4*>(T + (size_t)(y1 * S + j) * C);
+        l0[q] = 1.f - ly;
+        l1[q] = ly;
+      } else {
+        int iA, iB, xs, xe;
+        ctx_pool_cols(S, y, a.H, iA, iB);
+        ctx_pool_bin(j, S, a.W, xs, xe);
+        const float* D = a.ctab0 + ((size_t)n * 50 + off) * C + ct * TCH + c4 * 4;
+        int ys, ye;
+        ctx_pool_bin(iA, S, a.H, ys, ye);
+        l0[q] = 1.f / (float)((ye - ys) * (xe - xs));
+        p0[q] = *reinterpret_cast<const float4*>(D + (size_t)(iA * S + j) * C);
+        if (iB >= 0) {
+          ctx_pool_bin(iB, S, a.H, ys, ye);
+          l1[q] = 1.f / (float)((ye - ys) * (xe - xs));
+          p1[q] = *reinterpret_cast<const float4*>(D + (size_t)(iB * S + j) * C);
+        }
+      }
     }
   }
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int it = threadIdx.x + q * blockDim.x;
+  for (int q = 0; q < Q; ++q) {
+    const int it = threadIdx.x + q * NT;
     if (it < items) {
-      const int c4 = it & 15, rest = it >> 4, bin = rest % 12, lt = rest / 12;
-      const float ly = lyv[q], l0 = 1.f - ly;
-      *reinterpret_cast<float4*>(tab + ((size_t)lt * 12 + bin) * 64 + c4 * 4) =
-          make_float4(l0 * p0[q].x + ly * p1[q].x, l0 * p0[q].y + ly * p1[q].y, l0 * p0[q].z + ly * p1[q].z,
-                      l0 * p0[q].w + ly * p1[q].w);
+      const int c4 = it % G4, rest = it / G4;      // rest = lt * 12 + bin
+      *reinterpret_cast<float4*>(tab + (size_t)rest * TCH + c4 * 4) =
+          make_float4(l0[q] * p0[q].x + l1[q] * p1[q].x, l0[q] * p0[q].y + l1[q] * p1[q].y,
+                      l0[q] * p0[q].z + l1[q] * p1[q].z, l0[q] * p0[q].w + l1[q] * p1[q].w);
     }
-  }
-}
-
-// CTXB table: tab[(lr * 12 + bin) * 256 + cl] = sum over the pool cells (i, j(bin)) whose row bin contains row
-// rlo + lr of dave[cell][c] / cell area (cl = channel in the 256-channel tile)
-__device__ __forceinline__ void ctxb_build_tab(const ConvArgs2& a, float* tab, int ct, int rlo, int nr) {
-  const int C = a.cC;
-  for (int it = threadIdx.x; it < nr * 12 * 64; it += blockDim.x) {
-    const int c4 = it & 63, rest = it >> 6, bin = rest % 12, lr = rest / 12;
-    const int r = rlo + lr;
-    const int n = (int)fdiv((uint32_t)r, a.fdH), y = r - n * a.H;
-    int S, j, off;
-    ctx_scale_of_bin(bin, S, j, off);
-    int xs, xe;
-    ctx_pool_bin(j, S, a.W, xs, xe);
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int i = 0; i < S; ++i) {
-      int ys, ye;
-      ctx_pool_bin(i, S, a.H, ys, ye);
-      if (y < ys || y >= ye) continue;
-      const float inv = 1.f / (float)((ye - ys) * (xe - xs));
-      const float4 d = *reinterpret_cast<const float4*>(a.ctab0 + ((size_t)n * 50 + off + i * S + j) * C + ct * 256 +
-                                                        c4 * 4);
-      acc.x += d.x * inv; acc.y += d.y * inv; acc.z += d.z * inv; acc.w += d.w * inv;
-    }
-    *reinterpret_cast<float4*>(tab + ((size_t)lr * 12 + bin) * 256 + c4 * 4) = acc;
   }
 }
 
 template <int DT, int WC, int WP, int PW>
 __device__ __forceinline__ void ctxf_epilogue(const ConvArgs2& a, f32x4 (&acc)[4][4 * PW], const float* tab, int ct,
                                               int pt, int rlo, int wc, int wp, int fr, int fq) {
-  constexpr int TP = 64 * PW * WP, NF = 4 * PW;
+  constexpr int TP = 64 * PW * WP, NF = 4 * PW, TCH = 16 * WC;   // TCH: channels of the tile (= TC / 4)
   const int C = a.cC;
-  const int cl0 = wc * 16 + fq * 4;                 // this lane's first channel in the 64-channel tile
-  const int c0 = ct * 64 + cl0;
-  const int chb = ct * 256 + wc * 64 + fq * 16;     // this lane's first GEMM column (= 4 * c0)
+  const int cl0 = wc * 16 + fq * 4;                 // this lane's first channel in the tile
+  const int c0 = ct * TCH + cl0;
+  const int chb = ct * 64 * WC + wc * 64 + fq * 16; // this lane's first GEMM column (= 4 * c0)
   uint2 fvw[NF];
 #pragma unroll
   for (int i = 0; i < NF; ++i) {
@@ -648,12 +661,12 @@ __device__ __forceinline__ void ctxf_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
     const int m = pt * TP + wp * 64 * PW + i * 16 + fr;
     if (m >= a.M) continue;
     const int r = (int)fdiv((uint32_t)m, a.fdW), x = m - r * a.W;
-    const float* tr = tab + (size_t)(r - rlo) * 2 * 12 * 64 + cl0;
+    const float* tr = tab + (size_t)(r - rlo) * 2 * 12 * TCH + cl0;
     // T[si][j], U[si][j]: up(t), up(u) of the 4 scales at this pixel, channels c0 + j
     float T[4][4], U[4][4];
     {
       const float4 t = *reinterpret_cast<const float4*>(tr);
-      const float4 u = *reinterpret_cast<const float4*>(tr + 12 * 64);
+      const float4 u = *reinterpret_cast<const float4*>(tr + 12 * TCH);
       T[0][0] = t.x; T[0][1] = t.y; T[0][2] = t.z; T[0][3] = t.w;
       U[0][0] = u.x; U[0][1] = u.y; U[0][2] = u.z; U[0][3] = u.w;
     }
@@ -664,10 +677,10 @@ __device__ __forceinline__ void ctxf_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
       float lx;
       ctx_bil(S, x, a.W, x0, x1, lx);
       const float l0 = 1.f - lx;
-      const float4 t0 = *reinterpret_cast<const float4*>(tr + (bo + x0) * 64);
-      const float4 t1 = *reinterpret_cast<const float4*>(tr + (bo + x1) * 64);
-      const float4 u0 = *reinterpret_cast<const float4*>(tr + (12 + bo + x0) * 64);
-      const float4 u1 = *reinterpret_cast<const float4*>(tr + (12 + bo + x1) * 64);
+      const float4 t0 = *reinterpret_cast<const float4*>(tr + (bo + x0) * TCH);
+      const float4 t1 = *reinterpret_cast<const float4*>(tr + (bo + x1) * TCH);
+      const float4 u0 = *reinterpret_cast<const float4*>(tr + (12 + bo + x0) * TCH);
+      const float4 u1 = *reinterpret_cast<const float4*>(tr + (12 + bo + x1) * TCH);
       T[si][0] = l0 * t0.x + lx * t1.x; T[si][1] = l0 * t0.y + lx * t1.y;
       T[si][2] = l0 * t0.z + lx * t1.z; T[si][3] = l0 * t0.w + lx * t1.w;
       U[si][0] = l0 * u0.x + lx * u1.x; U[si][1] = l0 * u0.y + lx * u1.y;
@@ -696,21 +709,13 @@ __device__ __forceinline__ void ctxf_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
   }
 }
 
-// adaptive-pool column bins of scale S containing x: jA always, jB (or -1) when two bins overlap at x
-__device__ __forceinline__ void ctx_pool_cols(int S, int x, int L, int& jA, int& jB) {
-  jA = (x * S) / L;
-  jB = -1;
-  if (jA > 0 && ((jA * L + S - 1) / S) > x) jB = jA - 1;                 // end of bin jA - 1 reaches past x
-  else if (jA + 1 < S && ((jA + 1) * L) / S <= x) jB = jA + 1;           // bin jA + 1 starts at or before x
-}
-
 template <int DT, int WC, int WP, int PW>
 __device__ __forceinline__ void ctxb_epilogue(const ConvArgs2& a, f32x4 (&acc)[4][4 * PW], const float* tab, int ct,
                                               int pt, int rlo, int wc, int wp, int fr, int fq) {
-  constexpr int TP = 64 * PW * WP, NF = 4 * PW, HALF = 2;
+  constexpr int TP = 64 * PW * WP, NF = 4 * PW, HALF = 2, TC = 64 * WC;
   const int C = a.cC;
-  const int cl = wc * 64 + fq * 16;                 // this lane's first channel in the 256-channel tile
-  const int chb = ct * 256 + cl;
+  const int cl = wc * 64 + fq * 16;                 // this lane's first channel in the tile
+  const int chb = ct * TC + cl;
   // groups of 2 pixel fragments: the dcat / mask loads of a group are issued before its first store (more in
   // flight spills: the 128 accumulators are live throughout)
 #pragma unroll
@@ -736,7 +741,7 @@ __device__ __forceinline__ void ctxb_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
       const int m = pt * TP + wp * 64 * PW + i * 16 + fr;
       if (m >= a.M) continue;
       const int r = (int)fdiv((uint32_t)m, a.fdW), x = m - r * a.W;
-      const float* tr = tab + (size_t)(r - rlo) * 12 * 256 + cl;
+      const float* tr = tab + (size_t)(r - rlo) * 12 * TC + cl;
       float v[16];
       unpack8h<DT>(g0[ii], v);
       unpack8h<DT>(g1[ii], v + 8);
@@ -747,7 +752,7 @@ __device__ __forceinline__ void ctxb_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
       auto add_bin = [&](int bin, float wgt) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const float4 t = *reinterpret_cast<const float4*>(tr + bin * 256 + q * 4);
+          const float4 t = *reinterpret_cast<const float4*>(tr + bin * TC + q * 4);
           v[q * 4 + 0] += wgt * t.x; v[q * 4 + 1] += wgt * t.y; v[q * 4 + 2] += wgt * t.z; v[q * 4 + 3] += wgt * t.w;
         }
       };
@@ -1046,10 +1051,18 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
 
   frag8_t a0[4], b0[4 * PW], a1[4], b1[4 * PW];
   issue(0);
-  if constexpr (EPI == EPI_CTXF) {
-    // the up-sampling row tables, beside the staging ring (visible after the first barrier below)
-    const int rlo = (pt * TP) / a.W, rhi = (min(a.M, (pt + 1) * TP) - 1) / a.W;
-    ctxf_build_tab(a, reinterpret_cast<float*>(smem + 2 * STAGE), ct, rlo, rhi - rlo + 1);
+  // context epilogues: row tables beside the staging ring when the launch reserved room for them (a.cC flag bit),
+  // visible after the first barrier below
+  constexpr bool CTX = (EPI == EPI_CTXF || EPI == EPI_CTXB);
+  constexpr int CTX_Q = CTX ? (5 * (EPI == EPI_CTXF ? 24 : 12) * ((EPI == EPI_CTXF ? TC / 4 : TC) / 4) + NW * 64 - 1) /
+                                  (NW * 64)
+                            : 1;
+  const bool ctx_pro = CTX && a.ctx_prologue;
+  if constexpr (CTX) {
+    if (ctx_pro) {
+      const int rlo = (pt * TP) / a.W, rhi = (min(a.M, (pt + 1) * TP) - 1) / a.W;
+      ctx_build_tab<EPI, TC, NW * 64, CTX_Q>(a, reinterpret_cast<float*>(smem + 2 * STAGE), ct, rlo, rhi - rlo + 1);
+    }
   }
   if (nk > 1) {
     issue(1);
@@ -1105,21 +1118,18 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
   read((nk - 1) & 1, 1, a1, b1);
   mma(a0, b0, 0, 4 * PW);
   mma(a1, b1, 0, 4 * PW);
-  if constexpr (EPI == EPI_CTXF || EPI == EPI_CTXB) {
-    static_assert(WC == 4 && WP == 2 && PW == 2, "context epilogues: 256 x 256 tiles");
-    // the staging LDS is free once every wave's last fragment reads are done: it holds the tile's row tables
+  if constexpr (CTX) {
     const int rlo = (pt * TP) / a.W;
     const int rhi = (min(a.M, (pt + 1) * TP) - 1) / a.W;
-    if constexpr (EPI == EPI_CTXF) {
-      ctxf_epilogue<DT, WC, WP, PW>(a, acc, reinterpret_cast<const float*>(smem + 2 * STAGE), ct, pt, rlo, wc, wp,
-                                    fr, fq);
-    } else {
-      float* tab = reinterpret_cast<float*>(smem);
+    float* tab = reinterpret_cast<float*>(smem + (ctx_pro ? 2 * STAGE : 0));
+    if (!ctx_pro) {
+      // the staging LDS is free once every wave's last fragment reads are done
       __syncthreads();
-      ctxb_build_tab(a, tab, ct, rlo, rhi - rlo + 1);
+      ctx_build_tab<EPI, TC, NW * 64, CTX_Q>(a, tab, ct, rlo, rhi - rlo + 1);
       __syncthreads();
-      ctxb_epilogue<DT, WC, WP, PW>(a, acc, tab, ct, pt, rlo, wc, wp, fr, fq);
     }
+    if constexpr (EPI == EPI_CTXF) ctxf_epilogue<DT, WC, WP, PW>(a, acc, tab, ct, pt, rlo, wc, wp, fr, fq);
+    else ctxb_epilogue<DT, WC, WP, PW>(a, acc, tab, ct, pt, rlo, wc, wp, fr, fq);
     return;
   } else {
     glds_epilogue<DT, WC, WP, PW, EPI>(a, acc, ct, pt, wc, wp, fr, fq);
@@ -1129,15 +1139,23 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
 template <int DT, int WC, int WP, int PW, int EPI>
 static int launch_glds2(const ConvArgs2& a, hipStream_t s, int nb = 1) {
   constexpr int TC = 64 * WC, TP = 64 * PW * WP;
-  const size_t lds = 2 * (size_t)(TC + TP) * 128 + (EPI == EPI_CTXF ? kCtxfTabBytes : 0);
+  size_t lds = 2 * (size_t)(TC + TP) * 128;
+  ConvArgs2 b = a;
+  if (EPI == EPI_CTXF || EPI == EPI_CTXB) {
+    // room for the context row tables beside the ring when it fits one CU's LDS (else: built after the main loop)
+    const size_t tab = (size_t)ctx_tab_row_bytes(EPI, TC) * ctx_max_rows(TP, a.W);
+    b.ctx_prologue = (lds + tab <= 160 * 1024) ? 1 : 0;
+    if (b.ctx_prologue) lds += tab;
+    else if ((size_t)ctx_tab_row_bytes(EPI, TC) * ctx_max_rows(TP, a.W) > lds) return -15;
+  }
   auto kfn = conv_glds2_kernel<DT, WC, WP, PW, EPI>;
-  static bool attr = false;
-  if (!attr) {
+  static size_t attr_lds = 0;
+  if (lds > attr_lds) {
     CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    attr = true;
+    attr_lds = lds;
   }
   const int nct = a.Cout / TC, npt = (a.M + TP - 1) / TP;
-  hipLaunchKernelGGL(kfn, dim3(nct * npt, nb), dim3(64 * WC * WP), lds, s, a);
+  hipLaunchKernelGGL(kfn, dim3(nct * npt, nb), dim3(64 * WC * WP), lds, s, b);
   return (int)hipGetLastError();
 }
 
@@ -2122,12 +2140,16 @@ static int conv_ctx_impl(int fwd, const void* x, const void* w, const float* tab
   b.Cout = fwd ? 4 * C : C;
   b.fdW = make_fastdiv((uint32_t)W); b.fdH = make_fastdiv((uint32_t)H);
   b.ctab0 = tab0; b.ctab1 = tab1; b.cat = (bf16_t*)cat; b.cC = C;
+  // tiles: 256 x 256 (8 waves, one block per CU) or 128 x 128 (4 waves, 64 KB ring: two blocks per CU, one block's
+  // epilogue beside the other's main loop); CANNET_CTX_TILE{F,B} = 256 / 128 overrides
+  const char* ev = getenv(fwd ? "CANNET_CTX_TILEF" : "CANNET_CTX_TILEB");
+  const int tile = ev ? atoi(ev) : 256;
   if (fwd) {
     b.mask = nullptr; b.fvp = (const bf16_t*)fv;
-    return launch_glds2<DT, 4, 2, 2, EPI_CTXF>(b, s);
+    return tile == 128 ? launch_glds2<DT, 2, 2, 1, EPI_CTXF>(b, s) : launch_glds2<DT, 4, 2, 2, EPI_CTXF>(b, s);
   }
   b.mask = (const bf16_t*)fv;
-  return launch_glds2<DT, 4, 2, 2, EPI_CTXB>(b, s);
+  return tile == 128 ? launch_glds2<DT, 2, 2, 1, EPI_CTXB>(b, s) : launch_glds2<DT, 4, 2, 2, EPI_CTXB>(b, s);
 }
 
 // 3x3 / 1x1 conv + bias + ReLU with the 2x2/s2 max-pool fused into the epilogue: yp = pooled output,

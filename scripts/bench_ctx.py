@@ -52,11 +52,17 @@ def main():
     t = torch.randn(n, 50, c, device="cuda")
     u = torch.randn(n, 50, c, device="cuda")
     res["CTXF gemm"] = timeit(lambda: C.conv_ctx_fwd(fv, ex.ctx2cat_fwd, t, u))
+    os.environ["CANNET_CTX_TILEF"] = "128"
+    res["CTXF gemm 128x128 tiles"] = timeit(lambda: C.conv_ctx_fwd(fv, ex.ctx2cat_fwd, t, u))
+    os.environ.pop("CANNET_CTX_TILEF")
     res["plain 1x1 gemm fv x W2cat (EPI_NONE)"] = timeit(lambda: C.conv_igemm(fv, ex.ctx2cat_fwd, None, ksize=1,
                                                                                  epi=C.EPI_NONE))
     dg, rowacc = C.ctx_bwd_lin(dcat, sv["wts"], sv["u"])
     res["ctx_bwd_lin"] = timeit(lambda: C.ctx_bwd_lin(dcat, sv["wts"], sv["u"]))
     res["CTXB gemm"] = timeit(lambda: C.conv_ctx_bwd(dg, ex.ctx2cat_dgr, t, dcat, fv))
+    os.environ["CANNET_CTX_TILEB"] = "128"
+    res["CTXB gemm 128x128 tiles"] = timeit(lambda: C.conv_ctx_bwd(dg, ex.ctx2cat_dgr, t, dcat, fv))
+    os.environ.pop("CANNET_CTX_TILEB")
     res["plain 1x1 gemm dG x W2cat^T (EPI_NONE)"] = timeit(lambda: C.conv_igemm(dg, ex.ctx2cat_dgr, None, ksize=1,
                                                                                    epi=C.EPI_NONE))
     dw = torch.empty(4 * c, c, 1, 1, device="cuda")

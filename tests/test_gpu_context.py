@@ -74,8 +74,11 @@ def _run(monkeypatch, linear, n, h, w, seed):
     return e_fwd, e_dfv, e_w
 
 
+@pytest.mark.parametrize("tile", ["256", "128"])
 @pytest.mark.parametrize("n,h,w", [(2, 17, 65), (1, 12, 128), (2, 9, 96)])
-def test_context_linear_vs_fp32(monkeypatch, n, h, w):
+def test_context_linear_vs_fp32(monkeypatch, n, h, w, tile):
+    monkeypatch.setenv("CANNET_CTX_TILEF", tile)
+    monkeypatch.setenv("CANNET_CTX_TILEB", tile)
     e_fwd, e_dfv, e_w = _run(monkeypatch, True, n, h, w, seed=n * 100 + h)
     assert e_fwd < 5e-3, e_fwd
     assert e_dfv < 2e-2, e_dfv
