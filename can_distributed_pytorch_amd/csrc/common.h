@@ -207,6 +207,35 @@ __device__ __forceinline__ void load_w1_frags(const bf16_t* w1, frag8_t (&w1f)[2
                                                                                 kk * 32 + fq * 8));
 }
 
+// ---------------------------------------------------------------------------
+// LDS-DMA through inline asm.  With the __builtin_amdgcn_{global,raw_ptr_buffer}_load_lds builtins hipcc (ROCm
+// 7.2) knows an LDS write is in flight and, unable to tell the DMA's destination buffer from the one a later
+// ds_read reads, emits s_waitcnt vmcnt(0) before that read: in a ring that issues stage s+2 between the MFMAs of
+// stage s and the fragment reads of stage s+1, every stage then waits out the DMA it has just issued (its full
+// latency, twice per stage in the weight-gradient GEMM).  Issued as asm the DMA is invisible to hipcc's counters;
+// every kernel using these orders it itself: a counted s_waitcnt vmcnt(N) and an s_barrier before the first
+// ds_read of the staged buffer (cdna_hip_programming.md: M0 is written and restored inside the statement).
+// lds: the wave-uniform LDS byte address of the 1-KiB destination (lane l writes lds + 16 l).
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return __builtin_amdgcn_readfirstlane((unsigned)(size_t)(const __attribute__((address_space(3))) void*)p);
+}
+__device__ __forceinline__ void glds16(const void* gsrc, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void glds4(const void* gsrc, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t rsrc, unsigned voff, unsigned soff, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds) : "memory");
+}
+
 // TCOL = 64 (CO = 64 only): 4 waves, one per output row, 75 KB of LDS, so TWO
 // blocks share a CU and one block's halo fetch overlaps the other's MFMAs (the
 // 128-column block is alone on its CU: fetch, then compute, then store).

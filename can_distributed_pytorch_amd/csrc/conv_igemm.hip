@@ -835,7 +835,7 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds_kernel(ConvArgs2 a)
         }
         dst = sbase + A_BYTES + (gi - NIA) * 1024;
       }
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+      glds16(src, lds_addr(dst));
     }
   };
 
@@ -977,11 +977,11 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
     unsigned char* sbase = smem + buf * STAGE;
 #pragma unroll
     for (int j = p * GA / PARTS; j < (p + 1) * GA / PARTS; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(a.w + aoff[j] + i_k), (__attribute__((address_space(3))) void*)(sbase + (wave + NW * j) * 1024), 16, 0, 0);
+      glds16((const void*)(a.w + aoff[j] + i_k), lds_addr((sbase + (wave + NW * j) * 1024)));
 #pragma unroll
     for (int j = p * GB / PARTS; j < (p + 1) * GB / PARTS; ++j) {
       const void* src = ((bmask[j / 3] >> (9 * (j % 3) + i_tap)) & 1u) ? (const void*)(a.x + boff[j] + sh) : (const void*)a.zero;
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sbase + A_BYTES + (wave + NW * j) * 1024), 16, 0, 0);
+      glds16(src, lds_addr((sbase + A_BYTES + (wave + NW * j) * 1024)));
     }
     if (p == PARTS - 1 && ++i_tap == ntap) { i_tap = 0; i_c0 += 64; }
   };
@@ -1000,7 +1000,7 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
 #endif
 #pragma unroll
     for (int j = 0; j < GA; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(a.w + aoff[j] + i_k), (__attribute__((address_space(3))) void*)(sbase + (wave + NW * j) * 1024), 16, 0, 0);
+      glds16((const void*)(a.w + aoff[j] + i_k), lds_addr((sbase + (wave + NW * j) * 1024)));
 #if defined(CAN_PROBE) && CAN_PROBE == 1
     if (++i_tap == ntap) { i_tap = 0; i_c0 += 64; }
     return;
@@ -1008,7 +1008,7 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
       const void* src = ((bmask[j / 3] >> (9 * (j % 3) + i_tap)) & 1u) ? (const void*)(a.x + boff[j] + sh) : (const void*)a.zero;
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sbase + A_BYTES + (wave + NW * j) * 1024), 16, 0, 0);
+      glds16(src, lds_addr((sbase + A_BYTES + (wave + NW * j) * 1024)));
     }
     if (++i_tap == ntap) { i_tap = 0; i_c0 += 64; }
   };
@@ -1264,7 +1264,7 @@ conv_halo64_kernel(HaloConvArgs a) {
       const void* src = a.zero;
       if (hp < HPIX && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
         src = a.x + ((size_t)(n * a.H + ih) * a.W + iw) * 64 + (((lane & 7) ^ (hc & 7)) * 8);
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(halo + i * 1024), 16, 0, 0);
+      glds16(src, lds_addr((halo + i * 1024)));
     }
   }
   auto issue_w = [&](int t) {
@@ -1273,8 +1273,7 @@ conv_halo64_kernel(HaloConvArgs a) {
     for (int j = 0; j < GW; ++j) {
       const int r = (wave + NW * j) * 8 + (lane >> 3);
       const int lc = (lane & 7) ^ (r & 7);
-      __builtin_amdgcn_global_load_lds((const void*)(a.w + (size_t)perm_row(r) * 576 + t * 64 + lc * 8),
-                                       (__attribute__((address_space(3))) void*)(dst + (wave + NW * j) * 1024), 16, 0, 0);
+      glds16((const void*)(a.w + (size_t)perm_row(r) * 576 + t * 64 + lc * 8), lds_addr((dst + (wave + NW * j) * 1024)));
     }
   };
   issue_w(0);
@@ -1556,12 +1555,10 @@ __global__ void __launch_bounds__(512, 1) conv_ws64_kernel(HaloConvArgs a) {
       const bool row_in = ih >= 0 && ih < a.H;      // wave-uniform
       const bf16_t* rbase = a.x + ((ptrdiff_t)(n * a.H + ih) * a.W + ow0 - 1) * 64;
       const void* src = (row_in && v0) ? (const void*)(rbase + o0) : (const void*)a.zero;
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(buf + (hr * 9 + wave) * 1024),
-                                       16, 0, 0);
+      glds16(src, lds_addr((buf + (hr * 9 + wave) * 1024)));
       if (wave == hr) {                             // the 9th piece column: one row per wave 0 .. 5
         const void* src1 = (row_in && v1) ? (const void*)(rbase + o1) : (const void*)a.zero;
-        __builtin_amdgcn_global_load_lds(src1, (__attribute__((address_space(3))) void*)(buf + (hr * 9 + 8) * 1024),
-                                         16, 0, 0);
+        glds16(src1, lds_addr((buf + (hr * 9 + 8) * 1024)));
       }
     }
   };
@@ -1630,8 +1627,7 @@ __global__ void __launch_bounds__(512, 1) conv_ws64_kernel(HaloConvArgs a) {
           const void* src = ok ? (const void*)(reinterpret_cast<const unsigned char*>(a.img) +
                                                ((size_t)(n * a.H + ih) * a.W + iw) * 8 + (d & 1) * 4)
                                : (const void*)a.zero;
-          __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(imgraw + wj * 256), 4, 0,
-                                           0);
+          glds4(src, lds_addr((imgraw + wj * 256)));
         }
       }
     }

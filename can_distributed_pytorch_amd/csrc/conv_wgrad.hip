@@ -387,7 +387,7 @@ __global__ void __launch_bounds__(64 * WC * WK * WM, (WC * WK * WM >= 8) ? 1 : 2
         }
         dst = sbase + A_BYTES + (gi - NIA) * 1024;
       }
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+      glds16(src, lds_addr(dst));
     }
   };
 
@@ -639,14 +639,13 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
 #endif
 #pragma unroll
     for (int j = p * GA / parts; j < (p + 1) * GA / parts; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(dy_rsrc, (__attribute__((address_space(3))) void*)(sa.sbase + (wave + NW * j) * 1024),
-                                               16, (int)(aoff0 + j * astride), (int)sa.soff, 0, 0);
+      blds16(dy_rsrc, aoff0 + j * astride, sa.soff, lds_addr(sa.sbase + (wave + NW * j) * 1024));
 #pragma unroll
     for (int j = p * GB / parts; j < (p + 1) * GB / parts; ++j) {
       const int iw = sa.ow0 + dw + brow0 + j * BSTEP;
       const bool ok = sa.row_ok && ((unsigned)iw < (unsigned)a.W);
       const void* src = ok ? (const void*)(sa.xs + boff0 + j * bstride) : (const void*)a.zero;
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sa.sbase + A_BYTES + (wave + NW * j) * 1024), 16, 0, 0);
+      glds16(src, lds_addr(sa.sbase + A_BYTES + (wave + NW * j) * 1024));
     }
   };
   auto issue = [&](int st, int buf) { issue_part(stage_addr(st, buf), 0, 1); };
@@ -757,6 +756,211 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
     }
 }
 
+// ===========================================================================
+// v3 = v2's addressing (row-aligned stages, hoisted per-lane DMA offsets, dY
+// through a buffer resource) with a DEEPER ring: 32-pixel stages (one MFMA
+// K step) in an NBUF-deep LDS ring (32 KB per stage for 256 x 256 tiles),
+// NBUF stages issued ahead.  v2 keeps one 64-pixel stage in flight while it
+// computes the other (the DMA of stage s+2 has one stage of MFMA work,
+// ~2k cycles at full rate, to land: less than a loaded chip's LDS-DMA
+// latency, ~1.1 us; its waves sat 49 % of their cycles in s_waitcnt /
+// barrier waits, profiles/r2/pmc_conv_kernels.txt).  Here a stage issued in
+// iteration s is waited for in iteration s + NBUF - 1 (3-4 stages of MFMA
+// work later).  Per iteration: wait for stage s+1 -> barrier (stage s's
+// buffer is free: its fragments were read in iteration s-1) -> DMA of stage
+// s+NBUF into that buffer, one piece per group of 8 MFMAs, interleaved with
+// the 32 MFMAs of stage s and the fragment reads of stage s+1 (two register
+// sets).
+// ===========================================================================
+template <int DT, int WC, int WK, int KW, int NBUF>
+__global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds3_kernel(WgradArgs2 a) {
+  constexpr int NW = WC * WK;
+  constexpr int TCo = 64 * WC, TK = 64 * WK * KW;
+  constexpr int BKM = 32;                          // pixels per stage (one MFMA K step)
+  constexpr int RBA = TCo * 2, RBB = TK * 2;
+  constexpr int A_BYTES = BKM * RBA, B_BYTES = BKM * RBB;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int NIA = A_BYTES / 1024, NIB = B_BYTES / 1024;
+  constexpr int GA = NIA / NW, GB = NIB / NW;
+  constexpr int GP = GA + GB;                      // LDS-DMA pieces per wave per stage
+  static_assert(NIA % NW == 0 && NIB % NW == 0 && GA >= 1 && GB >= 1, "instruction split");
+  static_assert(RBB == 512 || RBB == 256, "B row = 256 or 128 k");
+  static_assert(NBUF >= 3, "ring depth");
+
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wave % WC, wk = wave / WC;
+
+  const int nco = a.Cout / TCo, nkt = a.K / TK;
+  const int ntile = nco * nkt;
+  const int bid = xcd_remap(blockIdx.x, ntile * a.S * a.nb);
+  const int tile = bid % ntile, slice = (bid / ntile) % a.S, bt = bid / (ntile * a.S);
+  const int co0 = (tile % nco) * TCo, k0 = (tile / nco) * TK;
+  const int mbeg = slice * a.mslice;
+  const int mend = min(a.M, mbeg + a.mslice);
+  const int nstage = (mend > mbeg) ? (mend - mbeg) / BKM : 0;    // M, mslice multiples of 64
+  const bf16_t* gdy = a.dy + bt * a.dy_bs;
+  const bf16_t* gx = a.x + bt * a.x_bs;
+
+  const __amdgpu_buffer_rsrc_t dy_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)gdy, (short)0, a.M * a.Cout * 2, 0x00020000);
+  constexpr int ASTEP = NW * 1024 / RBA, BSTEP = NW * 1024 / RBB;    // rows between a wave's pieces
+  static_assert(GA == 1 || ASTEP % 16 == 0, "piece stride must keep the row swizzle");
+  static_assert(GB == 1 || BSTEP % 16 == 0, "piece stride must keep the row swizzle");
+  unsigned aoff0;
+  {
+    const int byte = wave * 1024 + lane * 16;
+    const int row = byte / RBA;
+    const int lc16 = swz8b<RBA>(row, ((byte % RBA) / 16) * 2) >> 1;
+    aoff0 = (unsigned)(row * a.Cout + co0 + lc16 * 8) * 2u;
+  }
+  const unsigned astride = (unsigned)(ASTEP * a.Cout * 2);
+  const int tap = k0 / a.Cin;
+  int dh = 0, dw = 0;
+  if (a.ksize == 3) {
+    const int kh = (tap * 11) >> 5;
+    dh = (kh - 1) * a.dil;
+    dw = (tap - kh * 3 - 1) * a.dil;
+  }
+  const int ci0 = k0 - tap * a.Cin;
+  int boff0, brow0;
+  {
+    const int byte = wave * 1024 + lane * 16;
+    const int row = byte / RBB;
+    brow0 = row;
+    const int lc16 = swz8b<RBB>(row, ((byte % RBB) / 16) * 2) >> 1;
+    boff0 = (row + dh * a.W + dw) * a.Cin + ci0 + lc16 * 8;
+  }
+  const int bstride = BSTEP * a.Cin;
+
+  struct StageAddr {
+    unsigned soff;
+    const bf16_t* xs;
+    int ow0;
+    bool row_ok;
+    unsigned char* sbase;
+  };
+  auto stage_addr = [&](int st) -> StageAddr {
+    StageAddr sa;
+    const int m0 = mbeg + st * BKM;
+    const uint32_t q = fdiv((uint32_t)m0, a.fdW);
+    sa.ow0 = m0 - (int)q * a.W;
+    const int oh = (int)q - (int)fdiv(q, a.fdH) * a.H;
+    sa.row_ok = (unsigned)(oh + dh) < (unsigned)a.H;
+    sa.sbase = smem + (st % NBUF) * STAGE;
+    sa.soff = (unsigned)m0 * (unsigned)a.Cout * 2u;
+    sa.xs = gx + (size_t)m0 * a.Cin;
+    return sa;
+  };
+  // piece pc of a stage: A pieces 0..GA-1, then B pieces
+  auto issue_piece = [&](const StageAddr& sa, int pc) {
+    if (pc < GA) {
+      const int j = pc;
+      blds16(dy_rsrc, aoff0 + j * astride, sa.soff, lds_addr(sa.sbase + (wave + NW * j) * 1024));
+    } else {
+      const int j = pc - GA;
+      const int iw = sa.ow0 + dw + brow0 + j * BSTEP;
+      const bool ok = sa.row_ok && ((unsigned)iw < (unsigned)a.W);
+      const void* src = ok ? (const void*)(sa.xs + boff0 + j * bstride) : (const void*)a.zero;
+      glds16(src, lds_addr(sa.sbase + A_BYTES + (wave + NW * j) * 1024));
+    }
+  };
+
+  f32x4 acc[4][4 * KW];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4 * KW; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, qd = (lane & 15) >> 2, p = lane & 3;
+  auto rd = [&](const unsigned char* base, int rb_wide, int rb, int col0) -> frag8_t {
+    const int r0 = 8 * g + qd;
+    const int c8 = (col0 >> 2) + p;
+    const int s0 = rb_wide ? swz8b<256>(r0, c8) : swz8b<128>(r0, c8);
+    const int s1 = rb_wide ? swz8b<256>(r0 + 4, c8) : swz8b<128>(r0 + 4, c8);
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + r0 * rb + s0 * 8));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + (r0 + 4) * rb + s1 * 8));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(frag8_t, v);
+  };
+  auto read = [&](int st, frag8_t (&af)[4], frag8_t (&bfr)[4 * KW]) {
+    const unsigned char* Ab = smem + (st % NBUF) * STAGE;
+    const unsigned char* Bb = Ab + A_BYTES;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) af[j] = rd(Ab, RBA >= 256, RBA, wc * 64 + j * 16);
+#pragma unroll
+    for (int i = 0; i < 4 * KW; ++i) bfr[i] = rd(Bb, RBB >= 256, RBB, wk * 64 * KW + i * 16);
+  };
+  auto mma = [&](const frag8_t (&af)[4], const frag8_t (&bfr)[4 * KW], int i0, int i1) {
+#pragma unroll
+    for (int i = i0; i < i1; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[j][i] = mfma16<DT>(af[j], bfr[i], acc[j][i]);
+  };
+
+  if (nstage > 0) {
+    // prologue: stages 0 .. NBUF-1 in flight, wait for stage 0
+#pragma unroll
+    for (int s = 0; s < NBUF; ++s)
+      if (s < nstage) {
+        const StageAddr sa = stage_addr(s);
+#pragma unroll
+        for (int pc = 0; pc < GP; ++pc) issue_piece(sa, pc);
+      }
+    if (nstage >= NBUF) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" :: "n"((NBUF - 1) * GP) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    frag8_t a0[4], b0[4 * KW], a1[4], b1[4 * KW];
+    read(0, a0, b0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    // steady state: every stage issued NBUF ahead; counted waits leave NBUF-2 stages in flight
+    auto body = [&](int st, frag8_t (&ac)[4], frag8_t (&bc)[4 * KW], frag8_t (&an)[4], frag8_t (&bn)[4 * KW]) {
+      // stage st+1 landed (this wave's pieces: all but the NBUF-2 younger stages), then every wave's
+      if (st + 1 < nstage) {
+        if (st + NBUF - 1 < nstage) asm volatile("s_waitcnt vmcnt(%0)" :: "n"((NBUF - 2) * GP) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      asm volatile("s_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      const bool more = st + NBUF < nstage;
+      StageAddr sa;
+      if (more) sa = stage_addr(st + NBUF);          // into stage st's buffer (its fragments are in ac / bc)
+      // 4 groups of MFMAs of stage st; DMA pieces of stage st+NBUF and the reads of stage st+1 between them
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+#pragma unroll
+        for (int pc = gq * GP / 4; pc < (gq + 1) * GP / 4; ++pc)
+          if (more) issue_piece(sa, pc);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(ac, bc, gq * KW, (gq + 1) * KW);
+        __builtin_amdgcn_sched_barrier(0);
+        if (gq == 0 && st + 1 < nstage) read(st + 1, an, bn);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);          // lgkmcnt(0): stage st+1's fragments in registers
+    };
+    int st = 0;
+    for (; st + 1 < nstage; st += 2) {
+      body(st, a0, b0, a1, b1);
+      body(st + 1, a1, b1, a0, b0);
+    }
+    if (st < nstage) body(st, a0, b0, a1, b1);
+  }
+
+  const int fr = lane & 15, fq = lane >> 4;
+  float* slab = a.ws + ((size_t)bt * a.S + slice) * a.K * a.Cout;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4 * KW; ++i) {
+      const int k = k0 + wk * 64 * KW + i * 16 + fr;
+      const int co = co0 + wc * 64 + j * 16 + fq * 4;
+      *reinterpret_cast<f32x4*>(slab + (size_t)k * a.Cout + co) = acc[j][i];
+    }
+}
+
 // Bias gradient partials for the v2 path: part[b][co] = sum of dY rows of
 // chunk b (SB chunks, fixed order; wgrad_reduce sums the SB partials).  A
 // separate short launch with many blocks, so the GEMM grid stays whole rounds.
@@ -808,6 +1012,21 @@ __global__ void __launch_bounds__(256) bias_colsum_kernel(const bf16_t* __restri
       part[(size_t)blockIdx.x * Cout + cg * 8 + e2] = t;
     }
   }
+}
+
+template <int DT, int WC, int WK, int KW, int NBUF>
+static int launch_wgrad4(const WgradArgs2& a, hipStream_t s) {
+  constexpr int STAGE = 32 * (64 * WC + 64 * WK * KW) * 2;
+  const size_t lds = (size_t)NBUF * STAGE;
+  auto kfn = wgrad_glds3_kernel<DT, WC, WK, KW, NBUF>;
+  static bool attr = false;
+  if (!attr) {
+    CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  const int ntile = (a.Cout / (64 * WC)) * (a.K / (64 * WK * KW));
+  hipLaunchKernelGGL(kfn, dim3(ntile * a.S * a.nb), dim3(64 * WC * WK), lds, s, a);
+  return (int)hipGetLastError();
 }
 
 template <int DT, int WC, int WK, int KW>
@@ -918,7 +1137,7 @@ __global__ void __launch_bounds__(576, 1) wgrad_halo_kernel(HaloArgs a) {
           src = a.x + ((size_t)(n * a.H + yy) * a.W + xx) * a.Cin + ci0 + lc16 * 8;
         dst = sbase + DY_BYTES + (i - NID) * 1024;
       }
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+      glds16(src, lds_addr(dst));
     }
   };
   // F1: X2 = relu(conv1_1(img) + b1) of the stage's (HH x HW_) halo into the X image, in the layout the
@@ -1401,6 +1620,14 @@ extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, in
   return 0;
 }
 
+// ring depth of the 256 x 256 weight-gradient GEMM (CANNET_WGRAD_RING: 0 = v2 two 64-pixel stages, 4 / 5 = v3
+// ring of 32-pixel stages)
+static int wgrad_ring_depth() {
+  const char* e = getenv("CANNET_WGRAD_RING");
+  const int d = e ? atoi(e) : 0;
+  return (d == 4 || d == 5) ? d : 0;
+}
+
 static const can::bf16_t* zero_page() {
   static void* z = nullptr;
   if (!z) {
@@ -1489,7 +1716,10 @@ static int conv_wgrad_impl(const void* dy, const void* x, float* ws, float* wsb,
           }
           WgradArgs2 g = a;
           g.wsb = nullptr;
-          rc = launch_wgrad3<DT, 4, 2, 2>(g, s);
+          const int ring = wgrad_ring_depth();
+          if (ring == 5) rc = launch_wgrad4<DT, 4, 2, 2, 5>(g, s);
+          else if (ring == 4) rc = launch_wgrad4<DT, 4, 2, 2, 4>(g, s);
+          else rc = launch_wgrad3<DT, 4, 2, 2>(g, s);
         } else
           rc = launch_wgrad2<DT, 4, 2, 1, 2, 2, 2>(a, s);   // same tiles / slicing as cfg 7
         break;

@@ -496,3 +496,24 @@ def test_conv_dgrad_w1g_fused(n, h, w, beta, dtype):
     C.conv_wgrad(dx_ref, x4, dw2, db2, ksize=3, first=True, beta=beta)
     _close(dw, dw2, 5e-3)
     _close(db, db2, 5e-3)
+
+
+@pytest.mark.parametrize("ring", ["4", "5"])
+@pytest.mark.parametrize("n,h,w,ci,co,dil,k", [
+    (1, 6, 64, 256, 256, 1, 3), (2, 5, 128, 512, 256, 2, 3), (1, 3, 64, 1024, 512, 2, 3), (2, 7, 128, 512, 512, 1, 3),
+    (2, 4, 128, 512, 2048, 1, 1)])
+def test_wgrad_deep_ring_bitwise(n, h, w, ci, co, dil, k, ring, monkeypatch):
+    """v3 weight gradient (32-pixel stages in a 4- / 5-deep LDS-DMA ring, CANNET_WGRAD_RING) == v2 (two 64-pixel
+    stages) bitwise: the same MFMAs accumulate the same pixels in the same order per output element."""
+    from can_distributed_pytorch_amd.ops import conv as C
+    torch.manual_seed(31)
+    x = torch.randn(n, h, w, ci, device="cuda").to(torch.bfloat16)
+    dy = torch.randn(n, h, w, co, device="cuda").to(torch.bfloat16)
+    ws = C.WgradWorkspace("cuda")
+    dw0, db0 = torch.empty(co, ci, k, k, device="cuda"), torch.empty(co, device="cuda")
+    dw1, db1 = torch.empty_like(dw0), torch.empty_like(db0)
+    C.conv_wgrad(dy, x, dw0, db0, ksize=k, dil=dil, ws=ws)
+    monkeypatch.setenv("CANNET_WGRAD_RING", ring)
+    C.conv_wgrad(dy, x, dw1, db1, ksize=k, dil=dil, ws=ws)
+    torch.cuda.synchronize()
+    assert torch.equal(dw0, dw1) and torch.equal(db0, db1)
