@@ -549,6 +549,13 @@ class CANNetExecutor:
         dw2cat = self._dw2cat
         dsp = dscale.data_ptr() if dscale is not None else 0
 
+        # du_S += W2_S^T dt_S, then dave_S = W1_S^T du_S (fp32 cell GEMMs).  Both before the side-stream fork:
+        # forked first, the dW2cat weight gradient takes every CU (one 128-KB-LDS block each) and these two short
+        # launches wait ~190 us behind it on the critical path
+        self.C.ctx_gemm(1, dt.data_ptr(), 0, self._ctx2_ptrs(), du.data_ptr(), [], n, c, 1.0, 1.0, 0, st)
+        dave = torch.empty_like(du)
+        self.C.ctx_gemm(1, du.data_ptr(), 0, self._ctx1_ptrs(), dave.data_ptr(), [], n, c, 0.0, 1.0, 0, st)
+
         def ctx2_wgrad():
             # dW2_S = dG_S^T fv (one GEMM over the interleaved columns) + dt_S^T u_S (the t = W2 u term)
             C.conv_wgrad(dg, fv, dw2cat, None, ksize=1, ws=ws, beta=0.0, scale=scale, dscale=dscale)
@@ -557,8 +564,6 @@ class CANNetExecutor:
                             float(scale), dsp, self._stream())
             ready([self.ctx2_index[sc] for sc in CONTEXT_SCALES])
         self._on_side(side, ctx2_wgrad, hold, dg, fv, dt, u)
-        # du_S += W2_S^T dt_S, then dave_S = W1_S^T du_S (fp32 cell GEMMs)
-        self.C.ctx_gemm(1, dt.data_ptr(), 0, self._ctx2_ptrs(), du.data_ptr(), [], n, c, 1.0, 1.0, 0, st)
 
         def ctx1_wgrad():
             gws = [grads[self.ctx1_index[sc]] for sc in CONTEXT_SCALES]
@@ -569,8 +574,6 @@ class CANNetExecutor:
                             float(scale), dsp, self._stream())
             ready([self.ctx1_index[sc] for sc in CONTEXT_SCALES])
         self._on_side(side, ctx1_wgrad, hold, du, ave)
-        dave = torch.empty_like(du)
-        self.C.ctx_gemm(1, du.data_ptr(), 0, self._ctx1_ptrs(), dave.data_ptr(), [], n, c, 0.0, 1.0, 0, st)
         hold.append(rowacc)
         return C.conv_ctx_bwd(dg, self.ctx2cat_dgr, dave, dcat, fv)
 
