@@ -890,20 +890,27 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds_kernel(ConvArgs2 a)
 //    first half of stage s+1 is read (right after the barrier) while the
 //    second half's MFMAs run, so LDS read latency is never exposed at the
 //    head of an MFMA burst.
+// JW = 8 (cfg 26, CANNET_GLDS_W4=1): each wave owns 128 channels (8 A fragments) x 64*PW pixels, so a
+// 256 x 256 tile runs on 4 waves (one per SIMD, 256 fp32 accumulators in AGPRs) instead of 8: every B fragment
+// read from LDS feeds 8 MFMAs instead of 4 (LDS fragment bytes per FLOP -1/3); same LDS image, DMA and
+// epilogue, bitwise-equal results.  Measured 14-27 % SLOWER per layer (profiles/r3/ab_glds_four_wave.txt): with
+// one wave per SIMD nothing covers the DMA issue and the stage barrier, so the 8-wave layout stays the default.
 // ===========================================================================
-template <int DT, int WC, int WP, int PW, int EPI>
+template <int DT, int WC, int WP, int PW, int EPI, int JW = 4>
 __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a) {
+  static_assert(JW == 4 || JW == 8, "channel fragments per wave");
   if (blockIdx.y) {                               // batched launch: item blockIdx.y
     a.x += blockIdx.y * a.xbs;
     a.w += blockIdx.y * a.wbs;
     a.y += blockIdx.y * a.ybs;
   }
   constexpr int NW = WC * WP;
-  constexpr int TC = 64 * WC, TP = 64 * PW * WP;
+  constexpr int TC = 16 * JW * WC, TP = 64 * PW * WP;
   constexpr int A_BYTES = TC * 128, B_BYTES = TP * 128;
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int NIA = A_BYTES / 1024, NIB = B_BYTES / 1024;
   constexpr int GA = NIA / NW, GB = NIB / NW;
+  constexpr int JH = JW / 4;                      // 64-channel halves per wave
   static_assert(NIA % NW == 0 && NIB % NW == 0, "instruction split");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1013,25 +1020,27 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
     if (++i_tap == ntap) { i_tap = 0; i_c0 += 64; }
   };
 
-  f32x4 acc[4][4 * PW];
+  f32x4 acc[JH][4][4 * PW];
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int h = 0; h < JH; ++h)
 #pragma unroll
-    for (int i = 0; i < 4 * PW; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4 * PW; ++i) acc[h][j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fq = lane >> 4;
-  auto read = [&](int buf, int kk, frag8_t (&af)[4], frag8_t (&bfr)[4 * PW]) {
+  auto read = [&](int buf, int kk, frag8_t (&af)[JW], frag8_t (&bfr)[4 * PW]) {
     const uint4* As = reinterpret_cast<const uint4*>(smem + buf * STAGE);
     const uint4* Bs = reinterpret_cast<const uint4*>(smem + buf * STAGE + A_BYTES);
     const int chunk = kk * 4 + fq;
 #if defined(CAN_PROBE) && CAN_PROBE >= 3
-    for (int j = 0; j < 4; ++j) af[j] = __builtin_bit_cast(frag8_t, make_uint4(buf + lane, kk, j, 1));
+    for (int j = 0; j < JW; ++j) af[j] = __builtin_bit_cast(frag8_t, make_uint4(buf + lane, kk, j, 1));
     for (int i = 0; i < 4 * PW; ++i) bfr[i] = __builtin_bit_cast(frag8_t, make_uint4(buf, kk + lane, i, 1));
     return;
 #endif
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int row = wc * 64 + j * 16 + fr;
+    for (int j = 0; j < JW; ++j) {
+      const int row = wc * (16 * JW) + j * 16 + fr;
       af[j] = __builtin_bit_cast(frag8_t, As[row * 8 + swz(row, chunk)]);
     }
 #pragma unroll
@@ -1041,19 +1050,20 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
     }
   };
   // MFMAs over pixel fragments [i0, i1) (so the B fragments die in halves)
-  auto mma = [&](const frag8_t (&af)[4], const frag8_t (&bfr)[4 * PW], int i0, int i1) {
+  auto mma = [&](const frag8_t (&af)[JW], const frag8_t (&bfr)[4 * PW], int i0, int i1) {
 #pragma unroll
     for (int i = i0; i < i1; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[j][i] = mfma16<DT>(af[j], bfr[i], acc[j][i]);
+      for (int j = 0; j < JW; ++j)
+        acc[j >> 2][j & 3][i] = mfma16<DT>(af[j], bfr[i], acc[j >> 2][j & 3][i]);
   };
 
-  frag8_t a0[4], b0[4 * PW], a1[4], b1[4 * PW];
+  frag8_t a0[JW], b0[4 * PW], a1[JW], b1[4 * PW];
   issue(0);
   // context epilogues: row tables beside the staging ring when the launch reserved room for them (a.cC flag bit),
   // visible after the first barrier below
   constexpr bool CTX = (EPI == EPI_CTXF || EPI == EPI_CTXB);
+  static_assert(!CTX || JW == 4, "context epilogues: 64-channel waves");
   constexpr int CTX_Q = CTX ? (5 * (EPI == EPI_CTXF ? 24 : 12) * ((EPI == EPI_CTXF ? TC / 4 : TC) / 4) + NW * 64 - 1) /
                                   (NW * 64)
                             : 1;
@@ -1128,17 +1138,19 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
       ctx_build_tab<EPI, TC, NW * 64, CTX_Q>(a, tab, ct, rlo, rhi - rlo + 1);
       __syncthreads();
     }
-    if constexpr (EPI == EPI_CTXF) ctxf_epilogue<DT, WC, WP, PW>(a, acc, tab, ct, pt, rlo, wc, wp, fr, fq);
-    else ctxb_epilogue<DT, WC, WP, PW>(a, acc, tab, ct, pt, rlo, wc, wp, fr, fq);
+    if constexpr (EPI == EPI_CTXF) ctxf_epilogue<DT, WC, WP, PW>(a, acc[0], tab, ct, pt, rlo, wc, wp, fr, fq);
+    else ctxb_epilogue<DT, WC, WP, PW>(a, acc[0], tab, ct, pt, rlo, wc, wp, fr, fq);
     return;
   } else {
-    glds_epilogue<DT, WC, WP, PW, EPI>(a, acc, ct, pt, wc, wp, fr, fq);
+    // a JW = 8 wave is two 64-channel waves of the WC * JH x WP layout to the shared epilogue
+#pragma unroll
+    for (int h = 0; h < JH; ++h) glds_epilogue<DT, WC * JH, WP, PW, EPI>(a, acc[h], ct, pt, wc * JH + h, wp, fr, fq);
   }
 }
 
-template <int DT, int WC, int WP, int PW, int EPI>
+template <int DT, int WC, int WP, int PW, int EPI, int JW = 4>
 static int launch_glds2(const ConvArgs2& a, hipStream_t s, int nb = 1) {
-  constexpr int TC = 64 * WC, TP = 64 * PW * WP;
+  constexpr int TC = 16 * JW * WC, TP = 64 * PW * WP;
   size_t lds = 2 * (size_t)(TC + TP) * 128;
   ConvArgs2 b = a;
   if (EPI == EPI_CTXF || EPI == EPI_CTXB) {
@@ -1148,7 +1160,7 @@ static int launch_glds2(const ConvArgs2& a, hipStream_t s, int nb = 1) {
     if (b.ctx_prologue) lds += tab;
     else if ((size_t)ctx_tab_row_bytes(EPI, TC) * ctx_max_rows(TP, a.W) > lds) return -15;
   }
-  auto kfn = conv_glds2_kernel<DT, WC, WP, PW, EPI>;
+  auto kfn = conv_glds2_kernel<DT, WC, WP, PW, EPI, JW>;
   static size_t attr_lds = 0;
   if (lds > attr_lds) {
     CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -1946,19 +1958,24 @@ static int launch_glds(const ConvArgs2& a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// 256 x 256 tiles on 4 waves of 128 x 128 (cfg 26) instead of 8 waves of 64 x 128 (cfg 21); CANNET_GLDS_W4=1
+static bool glds_w4() {
+  const char* e = getenv("CANNET_GLDS_W4");
+  return e != nullptr && e[0] == '1';
+}
 // default LDS-DMA tile config: v2 (pipelined); 128 x 512 tiles measured faster for K <= 1152
 static int glds_default_cfg(int Cin, int Cout, int ksize) {
   const int ktot = ksize * ksize * Cin;
   return (Cout % 256 == 0) ? 21 : (Cout % 128 == 0) ? (ktot <= 1152 ? 25 : 22) : 23;
 }
 static int glds_cfg_tp(int cfg) {   // pixels per tile of a v2 config
-  return (cfg == 21 || cfg == 22) ? 256 : (cfg == 23 || cfg == 25) ? 512 : 0;
+  return (cfg == 21 || cfg == 22 || cfg == 26) ? 256 : (cfg == 23 || cfg == 25) ? 512 : 0;
 }
 // rows of the bias-partial matrix an LDS-DMA config writes: pixel tiles x waves along the pixels (0: none)
 static int glds_bpart_rows(int cfg, int M) {
   int tp = 0, wp = 0;
   switch (cfg) {
-    case 11: case 21: tp = 256; wp = 2; break;   // 256 ch x 256 px, 4 x 2 waves
+    case 11: case 21: case 26: tp = 256; wp = 2; break;   // 256 ch x 256 px, 4 x 2 waves (26: 2 x 2 waves)
     case 12: case 22: tp = 256; wp = 4; break;   // 128 x 256, 2 x 4
     case 13: case 23: tp = 512; wp = 8; break;   // 64 x 512, 1 x 8
     case 25: tp = 512; wp = 4; break;            // 128 x 512, 2 x 4 (2 fragments per wave)
@@ -1970,7 +1987,10 @@ static int glds_bpart_rows(int cfg, int M) {
 template <int DT, int EPI>
 static int dispatch_glds(const ConvArgs2& a, int tile_cfg, hipStream_t s, int nb = 1) {
   int cfg = tile_cfg;
-  if (cfg == 0) cfg = glds_default_cfg(a.Cin, a.Cout, a.ksize);
+  if (cfg == 0) {
+    cfg = glds_default_cfg(a.Cin, a.Cout, a.ksize);
+    if (cfg == 21 && glds_w4()) cfg = 26;
+  }
   if constexpr (EPI == EPI_POOLFWD) {
     const int tp = glds_cfg_tp(cfg);
     if (tp == 0 || (a.H & 1) || a.W % (tp / 2) || a.yp == nullptr) return -12;
@@ -1986,6 +2006,7 @@ static int dispatch_glds(const ConvArgs2& a, int tile_cfg, hipStream_t s, int nb
     case 22: if (a.Cout % 128) return -8; return launch_glds2<DT, 2, 4, 1, EPI>(a, s, nb);
     case 23: return launch_glds2<DT, 1, 8, 1, EPI>(a, s, nb);
     case 25: if (a.Cout % 128) return -8; return launch_glds2<DT, 2, 4, 2, EPI>(a, s, nb);   // 128 x 512, 160 KB LDS
+    case 26: if (a.Cout % 256) return -8; return launch_glds2<DT, 2, 2, 2, EPI, 8>(a, s, nb);  // 256 x 256, 4 waves
   }
   return -9;
 }

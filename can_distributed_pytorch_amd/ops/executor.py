@@ -410,11 +410,12 @@ class CANNetExecutor:
         side = self._side_stream()
         hold = []          # operands of side-stream work, kept alive until the join below
 
-        # CANNET_BIAS_FUSED=1: the data-gradient epilogues also sum the bias gradient of the dY they write, so
-        # the weight-gradient launch need not re-read dY for db.  Off by default: measured 421-423 vs 427 img/s
-        # (profiles/r2/README.md) — folding the ~10^4 - 10^5 partial rows needs a short extra launch, and any
-        # short launch waits for CUs behind the one-block-per-CU GEMMs of the other stream (50-100 us each)
-        fuse_bias = os.environ.get("CANNET_BIAS_FUSED", "0") == "1"
+        # the data-gradient epilogues also sum the bias gradient of the dY they write, so the weight-gradient
+        # launch need not re-read dY for db (the bias column sums were ~1 ms/step of weight-gradient-stream
+        # time).  Round 2 measured it negative (421-423 vs 427 img/s, profiles/r2/README.md); after the round-3
+        # kernel changes it is ahead in every interleaved round (485.5-485.8 vs 483.3-485.1 img/s,
+        # profiles/r3/ab_bias_fused.txt), so it is the default; CANNET_BIAS_FUSED=0 re-reads dY
+        fuse_bias = os.environ.get("CANNET_BIAS_FUSED", "1") == "1"
 
         def wg(spec_or_w, dy, x, ksize, dil, first, wi, bi, bp=None):
             # bp: bias partials of dy summed by the data-gradient epilogue that wrote it (None: the weight-

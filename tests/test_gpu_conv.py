@@ -37,6 +37,8 @@ def _close(a, b, tol=2e-2):
     (2, 3, 7, 64, 128, 3, 1, 31),
     # 128 x 512 tile (160 KB LDS)
     (1, 20, 40, 128, 128, 3, 1, 25), (2, 9, 13, 256, 128, 3, 2, 25), (1, 5, 7, 128, 384, 1, 1, 25),
+    # 256 x 256 tile on 4 waves of 128 x 128
+    (1, 20, 20, 128, 256, 3, 1, 26), (2, 16, 24, 512, 512, 1, 1, 26), (2, 32, 32, 256, 512, 3, 2, 26),
 ])
 def test_conv_fwd(n, h, w, ci, co, k, dil, tile):
     from can_distributed_pytorch_amd.ops import conv as C
@@ -517,3 +519,44 @@ def test_wgrad_deep_ring_bitwise(n, h, w, ci, co, dil, k, ring, monkeypatch):
     C.conv_wgrad(dy, x, dw1, db1, ksize=k, dil=dil, ws=ws)
     torch.cuda.synchronize()
     assert torch.equal(dw0, dw1) and torch.equal(db0, db1)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("n,h,w,ci,co,k,dil", [(2, 8, 64, 256, 256, 3, 1), (1, 12, 16, 1024, 512, 3, 2),
+                                               (2, 16, 24, 512, 512, 1, 1), (1, 9, 13, 512, 256, 3, 2)])
+def test_glds_four_wave_tiles_bitwise(n, h, w, ci, co, k, dil, dtype, monkeypatch):
+    """256 x 256 tiles on 4 waves of 128 x 128 (CANNET_GLDS_W4=1, cfg 26) == the 8-wave layout (cfg 21), bitwise,
+    for every epilogue the default dispatch routes there: bias + ReLU, pool-fused forward, ReLU-mask data gradient
+    with bias partials, pool-backward data gradient, plain (same K order per output, same rounding)."""
+    from can_distributed_pytorch_amd.ops import conv as C
+    torch.manual_seed(31)
+    x = torch.randn(n, h, w, ci, device="cuda").to(dtype)
+    wt = (torch.randn(co, ci, k, k, device="cuda") * (2.0 / (k * k * ci)) ** 0.5).to(dtype).float()
+    b = torch.randn(co, device="cuda") * 0.1
+    wf = C.pack_weight_fwd(wt, dtype)
+    wdt = (torch.randn(ci, co, k, k, device="cuda") * 0.05).to(dtype).float()     # a co -> ci layer: dgrad ci -> co
+    wd = C.pack_weight_dgrad(wdt, dtype)
+    dy = torch.randn(n, h, w, ci, device="cuda").to(dtype)
+    mask = torch.randn(n, h, w, co, device="cuda").to(dtype)
+    full = torch.relu(torch.randn(n, 2 * h, 2 * w, co, device="cuda")).to(dtype)
+    full[:, ::3, ::2] = 0
+    _, codes = C.maxpool_codes(full)
+
+    def run():
+        r = [C.conv_igemm(x, wf, b, ksize=k, dil=dil),
+             C.conv_igemm(x, wf, None, ksize=k, dil=dil, epi=C.EPI_NONE)]
+        r += list(C.conv_dgrad_with_bias(dy, wd, ksize=k, dil=dil, epi=C.EPI_MASK, mask=mask))
+        if k == 3:
+            r += list(C.conv_dgrad_with_bias(dy, wd, ksize=3, dil=dil, epi=C.EPI_POOLBWD, mask=codes))
+        if C.conv_pool_fwd_ok(x, co, k):
+            r += list(C.conv_pool_fwd(x, wf, b, ksize=k, dil=dil, codes=True))
+        torch.cuda.synchronize()
+        return r
+
+    monkeypatch.delenv("CANNET_GLDS_W4", raising=False)
+    ref = run()
+    monkeypatch.setenv("CANNET_GLDS_W4", "1")
+    got = run()
+    assert len(got) == len(ref)
+    for g, r in zip(got, ref):
+        assert g is not None and torch.equal(g, r)
