@@ -1655,16 +1655,24 @@ static int conv_wgrad_impl(const void* dy, const void* x, float* ws, float* wsb,
   int Sb = S;                       // bias partials summed by the reduce kernel
   int Sb_ext = 0;
   const float* bsrc = wsb;          // bias partial rows the reduce kernel sums (external: bext itself when short)
+  // long external lists are folded to <= kBiasParts rows by a short launch queued AFTER the GEMM on this (weight-
+  // gradient) stream: it then takes the CUs the GEMM's last blocks release.  Queued on the data-gradient stream (the
+  // producer) it waited 85-345 us for CUs behind this stream's one-block-per-CU GEMM, on the critical path
+  // (profiles/r3/ab_bias_prereduce.txt)
+  int bias_rpb = 0;
   if (ext) {
     if (bext_rows <= kBiasParts) {
       bsrc = bext;
       Sb_ext = bext_rows;
     } else {
-      const int rpb = (bext_rows + kBiasParts - 1) / kBiasParts;
-      Sb_ext = (bext_rows + rpb - 1) / rpb;
-      hipLaunchKernelGGL(bias_rows_reduce_kernel, dim3(Sb_ext), dim3(256), 0, s, bext, wsb, bext_rows, Cout, rpb);
+      bias_rpb = (bext_rows + kBiasParts - 1) / kBiasParts;
+      Sb_ext = (bext_rows + bias_rpb - 1) / bias_rpb;
     }
   }
+  auto bias_pre = [&]() {
+    if (bias_rpb)
+      hipLaunchKernelGGL(bias_rows_reduce_kernel, dim3(Sb_ext), dim3(256), 0, s, bext, wsb, bext_rows, Cout, bias_rpb);
+  };
   if (first || cfg == 0) {
     if (Cin != 4 || Cout % 64) return -2;
     WgradArgs a;
@@ -1695,6 +1703,7 @@ static int conv_wgrad_impl(const void* dy, const void* x, float* ws, float* wsb,
       h.tiles_per_slice = (h.ntiles + S - 1) / S;
       rc = ring ? launch_halo_ring<DT, 64, 4>(h, s) : launch_halo<DT, 64, 2>(h, s);
       if (rc) return rc;
+      bias_pre();
       return ext ? launch_reduce2(ws, bsrc, dw, db, S, Sb_ext, K, Cout, Cin, 9, 0, beta, scale, dscale, s)
                  : launch_reduce2(ws, wsb_used, dw, db, S, S, K, Cout, Cin, 9, 0, beta, scale, dscale, s);
     }
@@ -1745,6 +1754,7 @@ static int conv_wgrad_impl(const void* dy, const void* x, float* ws, float* wsb,
     }
   }
   if (rc) return rc;
+  bias_pre();
   if (ext) return launch_reduce2(ws, bsrc, dw, db, S, Sb_ext, K, Cout, first ? 4 : Cin, ksize * ksize, first, beta,
                                  scale, dscale, s);
   return launch_reduce2(ws, wsb_used, dw, db, S, Sb, K, Cout, first ? 4 : Cin, ksize * ksize, first, beta, scale, dscale,

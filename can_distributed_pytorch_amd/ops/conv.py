@@ -192,10 +192,10 @@ def conv_dgrad_with_bias(dy: torch.Tensor, wpack: torch.Tensor, *, ksize: int, d
     co = wpack.shape[0]
     bp = torch.empty(bias_part_capacity(n, h, w), co, dtype=torch.float32, device=dy.device)
     out, part = conv_igemm(dy, wpack, None, ksize=ksize, dil=dil, epi=epi, mask=mask, tile=tile, bias_part=bp)
-    if part is not None and part.shape[0] > BIAS_ROWS:
-        # long partial lists (the halo kernel: one row per 4 x 64 tile slot) are folded right here, on the
-        # producer's stream where the CUs the dgrad just released are free; a short launch queued on the
-        # weight-gradient stream would wait for CUs behind the next data-gradient kernel
+    if part is not None and part.shape[0] > BIAS_ROWS and os.environ.get("CANNET_BIAS_PRE_MAIN", "0") == "1":
+        # CANNET_BIAS_PRE_MAIN=1: long partial lists folded right here, on the producer's (critical-path) stream.
+        # Default: conv_wgrad folds them on the weight-gradient stream after its GEMM; here the short launch waited
+        # 85-345 us for CUs behind the weight-gradient GEMM (profiles/r3/ab_bias_prereduce.txt)
         C = _ext.require()
         red = torch.empty(BIAS_ROWS, co, dtype=torch.float32, device=dy.device)
         g = C.bias_rows_reduce(part.data_ptr(), red.data_ptr(), part.shape[0], co, BIAS_ROWS,

@@ -368,7 +368,9 @@ def test_conv1_2_with_conv1_1_recomputed_is_bitwise_stored_path(n, h, w, dtype, 
 @pytest.mark.parametrize("n,h,w,ci,co,dil,epi", [
     (2, 12, 20, 128, 64, 1, "pool"), (1, 9, 13, 256, 128, 1, "pool"), (2, 6, 64, 512, 256, 1, "pool"),
     (2, 16, 96, 64, 64, 1, "mask"), (1, 10, 70, 128, 64, 1, "mask"), (2, 12, 128, 128, 128, 1, "mask"),
-    (2, 8, 64, 512, 512, 2, "mask"), (1, 5, 40, 256, 128, 2, "mask"), (2, 8, 128, 64, 128, 1, "mask")])
+    (2, 8, 64, 512, 512, 2, "mask"), (1, 5, 40, 256, 128, 2, "mask"), (2, 8, 128, 64, 128, 1, "mask"),
+    # > 512 partial rows: folded by the short launch conv_wgrad queues after its GEMM
+    (8, 96, 128, 256, 512, 2, "mask"), (4, 48, 128, 128, 256, 1, "pool")])
 def test_dgrad_bias_partials_feed_wgrad(n, h, w, ci, co, dil, epi, dtype):
     """The data-gradient epilogue's bias partials (EPI_MASK on the LDS-DMA and halo kernels, EPI_POOLBWD through
     the max-pool codes) reduce to the bias gradient of the tensor it writes: db from the partials == db from
