@@ -337,9 +337,14 @@ struct ConvArgs2 {
 
 // pixel m of row r of pixel tile pt; EPI_POOLFWD tiles are 2 rows x TP/2 columns, rows interleaved per
 // 16-pixel fragment (see EPI_POOLFWD), the other epilogues take TP consecutive pixels
-template <int TP, int EPI>
+// RT (row-ring kernel, conv_rring_kernel): a 256-pixel tile is 2 image rows x 128 columns, tile pt = (n, row pair,
+// 128-column block) with the column block fastest; r = row * 128 + column (W % 128 == 0, H even)
+template <int TP, int EPI, int RT = 0>
 __device__ __forceinline__ int tile_pix(const ConvArgs2& a, int pt, int r) {
-  if constexpr (EPI == EPI_POOLFWD) {
+  if constexpr (RT != 0 && EPI != EPI_POOLFWD) {
+    const int tx = a.W >> 7, q = pt / tx, cb = pt - q * tx;
+    return (2 * q + (r >> 7)) * a.W + cb * 128 + (r & 127);
+  } else if constexpr (EPI == EPI_POOLFWD) {
     const int ncb = a.W / (TP / 2);
     const int rp = pt / ncb, cb = pt - rp * ncb;    // rp = n * H/2 + pooled row
     return (2 * rp + (r & 1)) * a.W + cb * (TP / 2) + (r >> 4) * 8 + ((r & 15) >> 1);
@@ -350,7 +355,7 @@ __device__ __forceinline__ int tile_pix(const ConvArgs2& a, int pt, int r) {
 
 // Shared epilogue of the LDS-DMA kernels: lane (fr, fq) of wave (wc, wp) owns
 // 16 consecutive output channels of one pixel per 16x16 pixel fragment.
-template <int DT, int WC, int WP, int PW, int EPI>
+template <int DT, int WC, int WP, int PW, int EPI, int RT = 0>
 __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4][4 * PW], int ct, int pt,
                                               int wc, int wp, int fr, int fq) {
   constexpr int TC = 64 * WC, TP = 64 * PW * WP;
@@ -376,7 +381,7 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
   if constexpr (EPI == EPI_MASK || EPI == EPI_POOLBWD) {
 #pragma unroll
     for (int i = 0; i < NF; ++i) {
-      const int m = tile_pix<TP, EPI>(a, pt, wp * 64 * PW + i * 16 + fr);
+      const int m = tile_pix<TP, EPI, RT>(a, pt, wp * 64 * PW + i * 16 + fr);
       if constexpr (EPI == EPI_MASK) {
         mk0[i] = make_uint4(0u, 0u, 0u, 0u);
         mk1[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -396,7 +401,7 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
   }
 #pragma unroll
   for (int i = 0; i < 4 * PW; ++i) {
-    const int m = tile_pix<TP, EPI>(a, pt, wp * 64 * PW + i * 16 + fr);
+    const int m = tile_pix<TP, EPI, RT>(a, pt, wp * 64 * PW + i * 16 + fr);
     if (m >= a.M) continue;
     float v[16];
 #pragma unroll
@@ -1169,6 +1174,193 @@ static int launch_glds2(const ConvArgs2& a, hipStream_t s, int nb = 1) {
   const int nct = a.Cout / TC, npt = (a.M + TP - 1) / TP;
   hipLaunchKernelGGL(kfn, dim3(nct * npt, nb), dim3(64 * WC * WP), lds, s, b);
   return (int)hipGetLastError();
+}
+
+// ===========================================================================
+// Row-ring 3x3 conv (forward / data gradient; cfg 27): the 256 x 256 tile of conv_glds2 (8 waves of 64 channels x
+// 128 pixels, same MFMA order, same epilogue) with the activation operand staged once per input ROW instead of once
+// per tap.  A pixel tile is 2 image rows x 128 columns (W % 128 == 0, H even); for one 64-channel chunk its 9 taps
+// read only 2 + 2 * dil input rows, each a 128-column row plus an 8-pixel guard on both sides.  The rows sit in a
+// 4-slot LDS ring (18 KB each) beside the 2-stage weight ring: a row is DMA'd two stages ahead of its first tap
+// (with that stage's weights) into the slot of the row whose last tap is already in registers, and every tap reads
+// its shifted window from the row slots (chunk swizzle keyed on the slot pixel, conflict-free for any shift).
+// LDS-DMA per 64-deep stage: 32 KB weights + 7.1 (dil 1) / 10.7 (dil 2) KB of rows instead of 32 + 32 KB; the
+// weight and row pieces are issued between the MFMA groups like conv_glds2's.  Out-of-image rows and columns come
+// from the zero page (guards of a one-block-wide map are zeroed once).  Results are bitwise those of cfg 21.
+// ===========================================================================
+constexpr int RR_SLOT = 144 * 128;                         // 8-px guard | 128 columns | 8-px guard, 64 channels
+constexpr int RR_RING = 4;                                 // row slots (enough for dil 1 and 2, see the schedule)
+constexpr int RR_LDS = 2 * 256 * 128 + RR_RING * RR_SLOT;  // 139,264 B
+
+template <int DT, int EPI, int D>
+__global__ void __launch_bounds__(512, 1) conv_rring_kernel(ConvArgs2 a) {
+  static_assert(D == 1 || D == 2, "dilation 1 or 2");
+  static_assert(EPI != EPI_POOLFWD && EPI != EPI_CTXF && EPI != EPI_CTXB, "row-ring epilogues");
+  constexpr int WC = 4, NW = 8, TC = 256;
+  constexpr int A_BYTES = TC * 128;
+  constexpr int GA = A_BYTES / 1024 / NW;         // 4 weight pieces per wave per stage (one per MFMA group)
+  constexpr int NR = 2 + 2 * D;                   // input rows of a 2-row tile per channel chunk
+  static_assert(GA == 4, "one weight piece per MFMA group");
+
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* ring = smem + 2 * A_BYTES;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wave % WC, wp = wave / WC;       // wp = the tile row this wave computes
+
+  const int tx = a.W >> 7;
+  const int nct = a.Cout / TC;
+  const int npt = a.M >> 8;
+  const int tile = xcd_remap(blockIdx.x, nct * npt);
+  const int ct = tile % nct, pt = tile / nct;
+  const int q = pt / tx, cb = pt - q * tx;
+  const int grow0 = 2 * q;                                    // n * H + oh0
+  const int oh0 = grow0 - (int)fdiv((uint32_t)grow0, a.fdH) * a.H;
+  const int col0 = cb * 128;
+  const int Ktot = 9 * a.Cin;
+  const int nc = a.Cin >> 6, nk = 9 * nc;
+  const int lc8 = ((lane & 7) ^ (lane >> 3)) * 8;             // swizzled 16-B chunk (pieces are 8-pixel aligned)
+
+  int aoff[GA];
+#pragma unroll
+  for (int j = 0; j < GA; ++j) {
+    const int r = (wave + NW * j) * 8 + (lane >> 3);
+    aoff[j] = (ct * TC + perm_row(r)) * Ktot + lc8;
+  }
+  const int boff = (lane >> 3) * a.Cin + lc8;                 // lane's pixel / chunk inside a row piece
+
+  if (tx == 1) {
+    // the guards of a one-block-wide map are always zero padding: written once (4 slots x 16 pixels x 8 chunks)
+    const int sl = tid >> 7, g = (tid >> 3) & 15;
+    reinterpret_cast<uint4*>(ring + sl * RR_SLOT + ((g < 8) ? g : 128 + g) * 128)[tid & 7] = make_uint4(0u, 0u, 0u, 0u);
+  }
+
+  // stage s = 9 * chunk + tap (chunk-major, tap-minor: conv_glds2's k order); the weights of stage s and the rows
+  // whose first tap is stage s are issued together, two stages ahead.  Row r of chunk c (input row oh0 - D + r) is
+  // first read by tap 3 * max(0, r - D)... i.e. rows {0, 1} at tap 0, {2 .. 1 + D} at tap 3, {2 + D .. NR - 1} at
+  // tap 6, and last read at tap 3 * floor(r / D) + 2 (D = 1: rows 2, 3 both at tap 8): with 4 slots every slot's
+  // previous row has had its last tap at or before the issuing stage (whose fragments are in registers once the
+  // stage's barrier has passed).
+  auto issue_part = [&](int st, int buf, int p) {
+    const int c = st / 9, tap = st - 9 * c;
+    glds16((const void*)(a.w + aoff[p] + tap * a.Cin + c * 64), lds_addr(smem + buf * A_BYTES + (wave + NW * p) * 1024));
+    const int nr = (tap == 0) ? 2 : (tap == 3 || tap == 6) ? D : 0;
+    if (p < 2 * nr) {
+      const int r = ((tap == 0) ? 0 : (tap == 3) ? 2 : 2 + D) + (p >> 1);
+      const int ih = oh0 - D + r;
+      const bool rv = (unsigned)ih < (unsigned)a.H;
+      unsigned char* slot = ring + ((c * NR + r) & (RR_RING - 1)) * RR_SLOT;
+      const size_t rbase = ((size_t)(grow0 - D + r) * a.W + col0) * a.Cin + c * 64;
+      const int j = wave + NW * (p & 1);                       // interior piece: pixels 8j .. 8j + 7
+      glds16(rv ? (const void*)(a.x + rbase + (size_t)(8 * j) * a.Cin + boff) : (const void*)(a.zero + lane * 8),
+             lds_addr(slot + (j + 1) * 1024));
+      if (tx > 1 && (p & 1) == 0 && wave < 2) {
+        // 8-pixel guards of an interior column block: real pixels of the neighbouring blocks (wave 0 left, 1 right)
+        const bool gv = rv && (wave == 0 ? cb > 0 : cb + 1 < tx);
+        const long long gc = (wave == 0) ? -8 : 128;
+        glds16(gv ? (const void*)(a.x + (long long)rbase + gc * a.Cin + boff) : (const void*)(a.zero + lane * 8),
+               lds_addr(slot + (wave == 0 ? 0 : 17) * 1024));
+      }
+    }
+  };
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  auto read = [&](int st, int kk, frag8_t (&af)[4], frag8_t (&bfr)[8]) {
+    const uint4* As = reinterpret_cast<const uint4*>(smem + (st & 1) * A_BYTES);
+    const int chunk = kk * 4 + fq;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = wc * 64 + j * 16 + fr;
+      af[j] = __builtin_bit_cast(frag8_t, As[row * 8 + swz(row, chunk)]);
+    }
+    const int c = st / 9, tap = st - 9 * c, kh = (tap * 11) >> 5, kw = tap - 3 * kh;
+    const int hp = 8 + fr + (kw - 1) * D;          // slot pixel of this lane's column in fragment 0
+    const unsigned char* base =
+        ring + ((c * NR + kh * D + wp) & (RR_RING - 1)) * RR_SLOT + hp * 128 + ((chunk ^ (hp & 7)) << 4);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) bfr[i] = __builtin_bit_cast(frag8_t, *reinterpret_cast<const uint4*>(base + i * 2048));
+  };
+  auto mma = [&](const frag8_t (&af)[4], const frag8_t (&bfr)[8], int i0, int i1) {
+#pragma unroll
+    for (int i = i0; i < i1; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j][i] = mfma16<DT>(af[j], bfr[i], acc[j][i]);
+  };
+
+  frag8_t a0[4], b0[8], a1[4], b1[8];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) issue_part(0, 0, p);
+  if (nk > 1) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) issue_part(1, 1, p);          // stage 1: weights only (no row starts at tap 1)
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" :: "n"(GA) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  read(0, 0, a0, b0);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  for (int s = 0; s < nk - 1; ++s) {
+    const int buf = s & 1;
+    read(s, 1, a1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(a0, b0, 0, 8);
+    // this wave's reads of stage s are in registers, stage s + 1 (weights and rows) has landed
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0x0070);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    const bool more = s + 2 < nk;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      if (more) issue_part(s + 2, buf, g);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(a1, b1, 2 * g, 2 * g + 2);
+      __builtin_amdgcn_sched_barrier(0);
+      if (g == 1) read(s + 1, 0, a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+  }
+  read(nk - 1, 1, a1, b1);
+  mma(a0, b0, 0, 8);
+  mma(a1, b1, 0, 8);
+  glds_epilogue<DT, WC, 2, 2, EPI, 1>(a, acc, ct, pt, wc, wp, fr, fq);
+}
+
+// the row-ring kernel applies: 3x3, dilation 1 / 2, W % 128 == 0, H even, Cout % 256 == 0
+static bool rring_ok(int H, int W, int Cin, int Cout, int ksize, int dil, int epi) {
+  return ksize == 3 && (dil == 1 || dil == 2) && W % 128 == 0 && H % 2 == 0 && Cout % 256 == 0 && Cin % 64 == 0 &&
+         epi != EPI_POOLFWD && epi != EPI_SIGMOID && epi != EPI_CTXF && epi != EPI_CTXB;
+}
+// CANNET_RRING: 0 = off, 1 (default) = dilation-1 layers, 2 = every dilation.  Measured per layer at batch 8 x
+// 768 x 1024 (profiles/r3/ab_rring.txt): dilation 1 -1..-4 %, dilation 2 +1..+7 % (slower) vs cfg 21
+static int rring_mode() {
+  const char* e = getenv("CANNET_RRING");
+  return e == nullptr ? 1 : atoi(e);
+}
+
+template <int DT, int EPI>
+static int launch_rring(const ConvArgs2& a, hipStream_t s) {
+  if constexpr (EPI == EPI_POOLFWD || EPI == EPI_SIGMOID || EPI == EPI_CTXF || EPI == EPI_CTXB) {
+    return -16;
+  } else {
+    if (!rring_ok(a.H, a.W, a.Cin, a.Cout, a.ksize, a.dil, EPI)) return -16;
+    auto kfn = (a.dil == 1) ? conv_rring_kernel<DT, EPI, 1> : conv_rring_kernel<DT, EPI, 2>;
+    static bool attr[2] = {false, false};
+    if (!attr[a.dil - 1]) {
+      CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, RR_LDS));
+      attr[a.dil - 1] = true;
+    }
+    const int nct = a.Cout / 256, npt = a.M >> 8;
+    hipLaunchKernelGGL(kfn, dim3(nct * npt), dim3(512), RR_LDS, s, a);
+    return (int)hipGetLastError();
+  }
 }
 
 // ===========================================================================
@@ -1975,7 +2167,7 @@ static int glds_cfg_tp(int cfg) {   // pixels per tile of a v2 config
 static int glds_bpart_rows(int cfg, int M) {
   int tp = 0, wp = 0;
   switch (cfg) {
-    case 11: case 21: case 26: tp = 256; wp = 2; break;   // 256 ch x 256 px, 4 x 2 waves (26: 2 x 2 waves)
+    case 11: case 21: case 26: case 27: tp = 256; wp = 2; break;   // 256 ch x 256 px, 4 x 2 waves (26: 2 x 2)
     case 12: case 22: tp = 256; wp = 4; break;   // 128 x 256, 2 x 4
     case 13: case 23: tp = 512; wp = 8; break;   // 64 x 512, 1 x 8
     case 25: tp = 512; wp = 4; break;            // 128 x 512, 2 x 4 (2 fragments per wave)
@@ -2007,6 +2199,7 @@ static int dispatch_glds(const ConvArgs2& a, int tile_cfg, hipStream_t s, int nb
     case 23: return launch_glds2<DT, 1, 8, 1, EPI>(a, s, nb);
     case 25: if (a.Cout % 128) return -8; return launch_glds2<DT, 2, 4, 2, EPI>(a, s, nb);   // 128 x 512, 160 KB LDS
     case 26: if (a.Cout % 256) return -8; return launch_glds2<DT, 2, 2, 2, EPI, 8>(a, s, nb);  // 256 x 256, 4 waves
+    case 27: if (nb > 1) return -8; return launch_rring<DT, EPI>(a, s);                    // 256 x 256 row ring
   }
   return -9;
 }
@@ -2091,6 +2284,7 @@ static int conv_igemm_impl(const void* x, const void* w, const float* bias, cons
     if (!b.zero) return -10;
     if (epi == EPI_POOLBWD) { b.mask = nullptr; b.pcodes = (const uint32_t*)mask; }   // mask = max-pool codes
     b.H = H; b.W = W; b.Cin = Cin; b.Cout = Cout; b.ksize = ksize; b.dil = dil; b.M = a.M;
+    if (tile_cfg == 0 && rring_mode() >= dil && rring_ok(H, W, Cin, Cout, ksize, dil, epi)) tile_cfg = 27;
     if (bpart != nullptr) {
       const int rows = glds_bpart_rows(tile_cfg ? tile_cfg : glds_default_cfg(Cin, Cout, ksize), a.M);
       if (rows > 0 && rows <= bpart_cap) { b.bpart = bpart; if (bpart_rows) *bpart_rows = rows; }

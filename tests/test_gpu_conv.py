@@ -562,3 +562,59 @@ def test_glds_four_wave_tiles_bitwise(n, h, w, ci, co, k, dil, dtype, monkeypatc
     assert len(got) == len(ref)
     for g, r in zip(got, ref):
         assert g is not None and torch.equal(g, r)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("n,h,w,ci,co,dil", [(2, 8, 128, 256, 256, 1), (1, 12, 128, 1024, 512, 2),
+                                             (1, 6, 256, 128, 256, 1), (2, 10, 384, 64, 256, 2),
+                                             (1, 4, 256, 512, 512, 2), (1, 2, 128, 192, 256, 1)])
+def test_row_ring_conv_bitwise(n, h, w, ci, co, dil, dtype, monkeypatch):
+    """Row-ring 3x3 conv (cfg 27: activation rows staged once per 64-channel chunk, taps read shifted windows of
+    the row slots) == the LDS-DMA 256 x 256 kernel (cfg 21, CANNET_RRING=0) bitwise for every epilogue it takes:
+    bias + ReLU, plain, bias, ReLU-mask data gradient with bias partials, pool-backward data gradient, fp32 store;
+    one- and multi-block-wide maps (zero guards / neighbour-pixel guards), dilation 1 and 2, top/bottom padding."""
+    from can_distributed_pytorch_amd.ops import conv as C
+    from can_distributed_pytorch_amd.ops import _ext
+    torch.manual_seed(37)
+    x = torch.randn(n, h, w, ci, device="cuda").to(dtype)
+    wt = (torch.randn(co, ci, 3, 3, device="cuda") * (2.0 / (9 * ci)) ** 0.5).to(dtype).float()
+    b = torch.randn(co, device="cuda") * 0.1
+    wf = C.pack_weight_fwd(wt, dtype)
+    wdt = (torch.randn(ci, co, 3, 3, device="cuda") * 0.05).to(dtype).float()     # a co -> ci layer: dgrad ci -> co
+    wd = C.pack_weight_dgrad(wdt, dtype)
+    mask = torch.randn(n, h, w, co, device="cuda").to(dtype)
+    full = torch.relu(torch.randn(n, 2 * h, 2 * w, co, device="cuda")).to(dtype)
+    full[:, ::3, ::2] = 0
+    _, codes = C.maxpool_codes(full)
+    ext = _ext.require()
+
+    def run():
+        r = [C.conv_igemm(x, wf, b, ksize=3, dil=dil),
+             C.conv_igemm(x, wf, None, ksize=3, dil=dil, epi=C.EPI_NONE),
+             C.conv_igemm(x, wf, b, ksize=3, dil=dil, epi=C.EPI_BIAS)]
+        r += list(C.conv_dgrad_with_bias(x, wd, ksize=3, dil=dil, epi=C.EPI_MASK, mask=mask))
+        r += list(C.conv_dgrad_with_bias(x, wd, ksize=3, dil=dil, epi=C.EPI_POOLBWD, mask=codes))
+        y32 = torch.empty(n, h, w, co, dtype=torch.float32, device="cuda")
+        ext.conv_igemm(x.data_ptr(), wf.data_ptr(), b.data_ptr(), 0, y32.data_ptr(), n, h, w, ci, co, 3, dil, 7, 0, 0,
+                       C.dt_code(dtype), _ext.stream_ptr(x.device), 0, 0)
+        r.append(y32)
+        torch.cuda.synchronize()
+        return r
+
+    monkeypatch.setenv("CANNET_RRING", "0")
+    ref = run()
+    monkeypatch.setenv("CANNET_RRING", "2")          # every dilation
+    got = run()
+    assert len(got) == len(ref)
+    for i, (g, r) in enumerate(zip(got, ref)):
+        assert g is not None
+        if i in (4, 6) and w > 128:
+            # bias partials: one row per (tile, wave row); a multi-block-wide map groups the pixels of a row-ring
+            # tile (2 rows x 128 columns) differently from a 256-pixel run, so only the column sums agree
+            torch.testing.assert_close(g.sum(0), r.sum(0), rtol=1e-4, atol=1e-3)
+        else:
+            assert torch.equal(g, r), f"output {i} differs"
+    # and against the fp32 reference (the cfg-21 path is covered there already; one direct check here)
+    yref = torch.relu(torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), wt, b, padding=dil,
+                                                 dilation=dil)).permute(0, 2, 3, 1)
+    _close(got[0].float(), yref, 2e-2)
