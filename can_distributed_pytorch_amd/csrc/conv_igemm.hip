@@ -987,9 +987,17 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
     sh += i_c0;
     const int i_k = i_tap * a.Cin + i_c0;
     unsigned char* sbase = smem + buf * STAGE;
+#if defined(CAN_PROBE) && CAN_PROBE >= 2
+    if (p == PARTS - 1 && ++i_tap == ntap) { i_tap = 0; i_c0 += 64; }
+    return;
+#endif
 #pragma unroll
     for (int j = p * GA / PARTS; j < (p + 1) * GA / PARTS; ++j)
       glds16((const void*)(a.w + aoff[j] + i_k), lds_addr((sbase + (wave + NW * j) * 1024)));
+#if defined(CAN_PROBE) && CAN_PROBE == 1
+    if (p == PARTS - 1 && ++i_tap == ntap) { i_tap = 0; i_c0 += 64; }
+    return;
+#endif
 #pragma unroll
     for (int j = p * GB / PARTS; j < (p + 1) * GB / PARTS; ++j) {
       const void* src = ((bmask[j / 3] >> (9 * (j % 3) + i_tap)) & 1u) ? (const void*)(a.x + boff[j] + sh) : (const void*)a.zero;
@@ -1095,7 +1103,9 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
     // this wave's reads of stage s are in registers, stage s+1 has landed
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_waitcnt(0x0070);
+#if !defined(CAN_PROBE) || CAN_PROBE < 4
     asm volatile("s_barrier" ::: "memory");
+#endif
     __builtin_amdgcn_sched_barrier(0);
 #ifndef CANNET_DMA_BURST
     if constexpr (PARTS > 1) {
@@ -1192,8 +1202,9 @@ constexpr int RR_SLOT = 144 * 128;                         // 8-px guard | 128 c
 constexpr int RR_RING = 4;                                 // row slots (enough for dil 1 and 2, see the schedule)
 constexpr int RR_LDS = 2 * 256 * 128 + RR_RING * RR_SLOT;  // 139,264 B
 
-template <int DT, int EPI, int D>
+template <int DT, int EPI, int D, int LEAD = 3>
 __global__ void __launch_bounds__(512, 1) conv_rring_kernel(ConvArgs2 a) {
+  static_assert(LEAD >= 3 && LEAD <= 4, "row lead: >= 3 (the counted barrier wait leaves the last rows in flight), <= 4 (4 ring slots)");
   static_assert(D == 1 || D == 2, "dilation 1 or 2");
   static_assert(EPI != EPI_POOLFWD && EPI != EPI_CTXF && EPI != EPI_CTXB, "row-ring epilogues");
   constexpr int WC = 4, NW = 8, TC = 256;
@@ -1235,32 +1246,58 @@ __global__ void __launch_bounds__(512, 1) conv_rring_kernel(ConvArgs2 a) {
     reinterpret_cast<uint4*>(ring + sl * RR_SLOT + ((g < 8) ? g : 128 + g) * 128)[tid & 7] = make_uint4(0u, 0u, 0u, 0u);
   }
 
-  // stage s = 9 * chunk + tap (chunk-major, tap-minor: conv_glds2's k order); the weights of stage s and the rows
-  // whose first tap is stage s are issued together, two stages ahead.  Row r of chunk c (input row oh0 - D + r) is
-  // first read by tap 3 * max(0, r - D)... i.e. rows {0, 1} at tap 0, {2 .. 1 + D} at tap 3, {2 + D .. NR - 1} at
-  // tap 6, and last read at tap 3 * floor(r / D) + 2 (D = 1: rows 2, 3 both at tap 8): with 4 slots every slot's
-  // previous row has had its last tap at or before the issuing stage (whose fragments are in registers once the
-  // stage's barrier has passed).
-  auto issue_part = [&](int st, int buf, int p) {
+  // stage s = 9 * chunk + tap (chunk-major, tap-minor: conv_glds2's k order).  The weights of stage s are issued two
+  // stages ahead (in the stage-(s-2) MFMA gaps, like conv_glds2), the rows whose first tap is stage f LEAD stages
+  // ahead, after that stage's weights: the barrier wait before stage s + 1 then counts only the row pieces just
+  // issued (vmcnt retires in order), so a row has LEAD - 1 stages to arrive (a first-touch row comes from beyond
+  // L2; with LEAD = 2 and a full vmcnt drain per stage the kernel waited on them).  Row r of chunk c (input row
+  // oh0 - D + r) is first read by tap 0 (rows 0, 1), 3 (rows 2 .. 1 + D) or 6 (the rest) and last read by tap
+  // 3 * floor(r / D) + 2 (D = 1: rows 2, 3 both by tap 8): with 4 slots and LEAD <= 4 every slot's previous row
+  // has had its last tap at or before the issuing stage, whose fragments are in registers once its barrier passed.
+  auto issue_A = [&](int st, int buf, int p) {
     const int c = st / 9, tap = st - 9 * c;
     glds16((const void*)(a.w + aoff[p] + tap * a.Cin + c * 64), lds_addr(smem + buf * A_BYTES + (wave + NW * p) * 1024));
-    const int nr = (tap == 0) ? 2 : (tap == 3 || tap == 6) ? D : 0;
-    if (p < 2 * nr) {
-      const int r = ((tap == 0) ? 0 : (tap == 3) ? 2 : 2 + D) + (p >> 1);
+  };
+  // row pieces this wave issues for the rows first read by stage f (0 when f is past the end)
+  auto row_pieces = [&](int f) -> int {
+    const int c = f / 9, tap = f - 9 * c;
+    const int nr = (c >= nc) ? 0 : (tap == 0) ? 2 : (tap == 3 || tap == 6) ? D : 0;
+    return nr * (2 + ((tx > 1 && wave < 2) ? 1 : 0));
+  };
+  auto issue_rows = [&](int f) {
+    const int c = f / 9, tap = f - 9 * c;
+    const int nr = (c >= nc) ? 0 : (tap == 0) ? 2 : (tap == 3 || tap == 6) ? D : 0;
+    for (int k = 0; k < nr; ++k) {
+      const int r = ((tap == 0) ? 0 : (tap == 3) ? 2 : 2 + D) + k;
       const int ih = oh0 - D + r;
       const bool rv = (unsigned)ih < (unsigned)a.H;
       unsigned char* slot = ring + ((c * NR + r) & (RR_RING - 1)) * RR_SLOT;
       const size_t rbase = ((size_t)(grow0 - D + r) * a.W + col0) * a.Cin + c * 64;
-      const int j = wave + NW * (p & 1);                       // interior piece: pixels 8j .. 8j + 7
-      glds16(rv ? (const void*)(a.x + rbase + (size_t)(8 * j) * a.Cin + boff) : (const void*)(a.zero + lane * 8),
-             lds_addr(slot + (j + 1) * 1024));
-      if (tx > 1 && (p & 1) == 0 && wave < 2) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int j = wave + NW * h;                           // interior piece: pixels 8j .. 8j + 7
+        glds16(rv ? (const void*)(a.x + rbase + (size_t)(8 * j) * a.Cin + boff) : (const void*)(a.zero + lane * 8),
+               lds_addr(slot + (j + 1) * 1024));
+      }
+      if (tx > 1 && wave < 2) {
         // 8-pixel guards of an interior column block: real pixels of the neighbouring blocks (wave 0 left, 1 right)
         const bool gv = rv && (wave == 0 ? cb > 0 : cb + 1 < tx);
         const long long gc = (wave == 0) ? -8 : 128;
         glds16(gv ? (const void*)(a.x + (long long)rbase + gc * a.Cin + boff) : (const void*)(a.zero + lane * 8),
                lds_addr(slot + (wave == 0 ? 0 : 17) * 1024));
       }
+    }
+  };
+  // s_waitcnt vmcnt(n) for a wave-uniform run-time n (the row pieces issued after the weights)
+  auto wait_vm = [&](int n) {
+    switch (n) {
+      case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+      case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+      case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+      case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+      case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+      case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+      default: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
     }
   };
 
@@ -1294,31 +1331,39 @@ __global__ void __launch_bounds__(512, 1) conv_rring_kernel(ConvArgs2 a) {
   };
 
   frag8_t a0[4], b0[8], a1[4], b1[8];
+  // prologue: every row first read before stage LEAD, the weights of stages 0 and 1, then a full drain
 #pragma unroll
-  for (int p = 0; p < 4; ++p) issue_part(0, 0, p);
+  for (int f = 0; f < LEAD; ++f) issue_rows(f);
+#pragma unroll
+  for (int p = 0; p < 4; ++p) issue_A(0, 0, p);
   if (nk > 1) {
 #pragma unroll
-    for (int p = 0; p < 4; ++p) issue_part(1, 1, p);          // stage 1: weights only (no row starts at tap 1)
-    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" :: "n"(GA) : "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    for (int p = 0; p < 4; ++p) issue_A(1, 1, p);
   }
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   read(0, 0, a0, b0);
   __builtin_amdgcn_s_waitcnt(0xC07F);
+  int rp_prev = 0;               // row pieces issued after the weights in the previous stage (still in flight)
   for (int s = 0; s < nk - 1; ++s) {
     const int buf = s & 1;
     read(s, 1, a1, b1);
     __builtin_amdgcn_sched_barrier(0);
     mma(a0, b0, 0, 8);
-    // this wave's reads of stage s are in registers, stage s + 1 (weights and rows) has landed
+    // this wave's reads of stage s are in registers; stage s + 1 (weights, rows) has landed: everything but the
+    // row pieces issued last stage
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_waitcnt(0x0070);
+    wait_vm(rp_prev);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
     asm volatile("s_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     const bool more = s + 2 < nk;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      if (more) issue_part(s + 2, buf, g);
+      if (more) issue_A(s + 2, buf, g);
+      if (g == 3) {
+        issue_rows(s + LEAD);
+        rp_prev = row_pieces(s + LEAD);
+      }
       __builtin_amdgcn_sched_barrier(0);
       mma(a1, b1, 2 * g, 2 * g + 2);
       __builtin_amdgcn_sched_barrier(0);
@@ -1338,8 +1383,10 @@ static bool rring_ok(int H, int W, int Cin, int Cout, int ksize, int dil, int ep
   return ksize == 3 && (dil == 1 || dil == 2) && W % 128 == 0 && H % 2 == 0 && Cout % 256 == 0 && Cin % 64 == 0 &&
          epi != EPI_POOLFWD && epi != EPI_SIGMOID && epi != EPI_CTXF && epi != EPI_CTXB;
 }
-// CANNET_RRING: 0 = off, 1 (default) = dilation-1 layers, 2 = every dilation.  Measured per layer at batch 8 x
-// 768 x 1024 (profiles/r3/ab_rring.txt): dilation 1 -1..-4 %, dilation 2 +1..+7 % (slower) vs cfg 21
+// CANNET_RRING: 0 = off, 1 (default) = dilation-1 layers, 2 = every dilation.  Per layer at batch 8 x 768 x 1024
+// (profiles/r3/ab_rring.txt) -2..-6 % vs cfg 21 with the rows issued 3 stages ahead (issued 2 ahead with a full
+// DMA drain per stage: dilation 1 -1..-4 %, dilation 2 +1..+7 %); the step: off 482.6, dilation 1 485.4, every
+// dilation 484.9 img/s (medians of 4 interleaved rounds)
 static int rring_mode() {
   const char* e = getenv("CANNET_RRING");
   return e == nullptr ? 1 : atoi(e);
@@ -1351,11 +1398,17 @@ static int launch_rring(const ConvArgs2& a, hipStream_t s) {
     return -16;
   } else {
     if (!rring_ok(a.H, a.W, a.Cin, a.Cout, a.ksize, a.dil, EPI)) return -16;
-    auto kfn = (a.dil == 1) ? conv_rring_kernel<DT, EPI, 1> : conv_rring_kernel<DT, EPI, 2>;
-    static bool attr[2] = {false, false};
-    if (!attr[a.dil - 1]) {
+    // CANNET_RRING_LEAD: stages a row is issued ahead of its first tap (3 or 4, default 3; per layer 3 measured
+    // 0.4 % ahead of 4, profiles/r3/ab_rring.txt)
+    const char* le = getenv("CANNET_RRING_LEAD");
+    const int lead = (le && atoi(le) == 4) ? 4 : 3;
+    auto kfn = (a.dil == 1) ? (lead == 4 ? conv_rring_kernel<DT, EPI, 1, 4> : conv_rring_kernel<DT, EPI, 1, 3>)
+                            : (lead == 4 ? conv_rring_kernel<DT, EPI, 2, 4> : conv_rring_kernel<DT, EPI, 2, 3>);
+    static const void* attr_done[4] = {};
+    const int ai = (a.dil - 1) * 2 + (lead == 4 ? 1 : 0);
+    if (attr_done[ai] != (const void*)kfn) {
       CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, RR_LDS));
-      attr[a.dil - 1] = true;
+      attr_done[ai] = (const void*)kfn;
     }
     const int nct = a.Cout / 256, npt = a.M >> 8;
     hipLaunchKernelGGL(kfn, dim3(nct * npt), dim3(512), RR_LDS, s, a);

@@ -10,19 +10,21 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 from can_distributed_pytorch_amd.ops import conv as C  # noqa: E402
 
+TILE = int(os.environ.get("PROBE_TILE", "21"))   # 21: conv_glds2 256 x 256 (27: row ring, no probe hooks)
 SHAPES = [("F9", 512, 512, 96, 128, 1), ("B1", 1024, 512, 96, 128, 2), ("F6", 256, 256, 192, 256, 1)]
 
 
 def main():
     libs = {}
-    for m in range(4):
-        lib = ctypes.CDLL(os.path.join(ROOT, "build", "probe", f"conv_probe{m}.so"))
+    for m in range(int(os.environ.get("PROBE_MODES", "4"))):
+        lib = ctypes.CDLL(os.path.join(os.environ.get("PROBE_DIR", os.path.join(ROOT, "build", "probe")), f"conv_probe{m}.so"))
         f = lib.can_conv_igemm
         f.restype = ctypes.c_int
-        f.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int] * 11 + [ctypes.c_void_p]
+        f.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int] * 11 + [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                                                    ctypes.c_void_p]
         libs[m] = f
     n = 8
-    for name, ci, co, h, w, dil in SHAPES:
+    for name, ci, co, h, w, dil in SHAPES * 3:
         x = torch.randn(n, h, w, ci, device="cuda").to(torch.bfloat16)
         wt = (torch.randn(co, ci, 3, 3, device="cuda") * 0.02)
         wp = C.pack_weight_fwd(wt)
@@ -32,8 +34,8 @@ def main():
         res = []
         for m, f in libs.items():
             def call():
-                rc = f(x.data_ptr(), wp.data_ptr(), b.data_ptr(), 0, y.data_ptr(), n, h, w, ci, co, 3, dil, 0, 0, 0,
-                       0, st)
+                rc = f(x.data_ptr(), wp.data_ptr(), b.data_ptr(), 0, y.data_ptr(), n, h, w, ci, co, 3, dil, 0, 0, TILE,
+                       0, st, None, 0, None)
                 assert rc == 0, rc
             for _ in range(3):
                 call()
