@@ -207,6 +207,13 @@ __device__ __forceinline__ void load_w1_frags(const bf16_t* w1, frag8_t (&w1f)[2
                                                                                 kk * 32 + fq * 8));
 }
 
+// LDS-DMA part placement in the MFMA groups of a stage's second K half (conv_glds2, conv_rring, wgrad_glds2), a
+// compile-time switch for A/B builds (-DCANNET_DMA_ORDER_CT=n; a run-time switch pushed the 256 x 256 kernels into
+// scratch): 0 = part g before group g, 1 = part g after group g, 2 = parts 0 / 1 after groups 0 / 1, 2 + 3 after 2
+#ifndef CANNET_DMA_ORDER_CT
+#define CANNET_DMA_ORDER_CT 0
+#endif
+
 // ---------------------------------------------------------------------------
 // LDS-DMA through inline asm.  With the __builtin_amdgcn_{global,raw_ptr_buffer}_load_lds builtins hipcc (ROCm
 // 7.2) knows an LDS write is in flight and, unable to tell the DMA's destination buffer from the one a later

@@ -337,13 +337,13 @@ struct ConvArgs2 {
 
 // pixel m of row r of pixel tile pt; EPI_POOLFWD tiles are 2 rows x TP/2 columns, rows interleaved per
 // 16-pixel fragment (see EPI_POOLFWD), the other epilogues take TP consecutive pixels
-// RT (row-ring kernel, conv_rring_kernel): a 256-pixel tile is 2 image rows x 128 columns, tile pt = (n, row pair,
-// 128-column block) with the column block fastest; r = row * 128 + column (W % 128 == 0, H even)
+// RT (row-ring kernel, conv_rring_kernel): a tile is RT image rows x 128 columns, tile pt = (n, row group, 128-column
+// block) with the column block fastest; r = row * 128 + column (W % 128 == 0, H % RT == 0)
 template <int TP, int EPI, int RT = 0>
 __device__ __forceinline__ int tile_pix(const ConvArgs2& a, int pt, int r) {
   if constexpr (RT != 0 && EPI != EPI_POOLFWD) {
     const int tx = a.W >> 7, q = pt / tx, cb = pt - q * tx;
-    return (2 * q + (r >> 7)) * a.W + cb * 128 + (r & 127);
+    return (RT * q + (r >> 7)) * a.W + cb * 128 + (r & 127);
   } else if constexpr (EPI == EPI_POOLFWD) {
     const int ncb = a.W / (TP / 2);
     const int rp = pt / ncb, cb = pt - rp * ncb;    // rp = n * H/2 + pooled row
@@ -1112,11 +1112,17 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
       // the four MFMA groups of the second K half, DMA parts of stage s+2 between them, the reads of stage
       // s+1's first half after the second group
       const bool more = s + 2 < nk;
+      constexpr int ord = CANNET_DMA_ORDER_CT;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        if ((g * PARTS) % 4 == 0 && more) issue_part(buf, g * PARTS / 4);
+        if (ord == 0 && more) issue_part(buf, g);
         __builtin_amdgcn_sched_barrier(0);
         mma(a1, b1, g * PW, (g + 1) * PW);
+        __builtin_amdgcn_sched_barrier(0);
+        if (ord != 0 && more && (ord == 1 || g < 3)) {
+          issue_part(buf, g);
+          if (ord == 2 && g == 2) issue_part(buf, 3);
+        }
         __builtin_amdgcn_sched_barrier(0);
         if (g == 1) read(buf ^ 1, 0, a0, b0);
         __builtin_amdgcn_sched_barrier(0);
@@ -1199,33 +1205,46 @@ static int launch_glds2(const ConvArgs2& a, hipStream_t s, int nb = 1) {
 // from the zero page (guards of a one-block-wide map are zeroed once).  Results are bitwise those of cfg 21.
 // ===========================================================================
 constexpr int RR_SLOT = 144 * 128;                         // 8-px guard | 128 columns | 8-px guard, 64 channels
-constexpr int RR_RING = 4;                                 // row slots (enough for dil 1 and 2, see the schedule)
-constexpr int RR_LDS = 2 * 256 * 128 + RR_RING * RR_SLOT;  // 139,264 B
+// LDS of a row-ring config: 2 weight stages + the row slots (TC = 256, 2-row tiles: 4 slots, 139,264 B; TC = 64,
+// 4-row tiles: 8 slots, 163,840 B = all of a CU's LDS)
+__host__ __device__ constexpr int rr_ring(int TR) { return TR == 2 ? 4 : 8; }
+__host__ __device__ constexpr int rr_lds(int TC, int TR) { return 2 * TC * 128 + rr_ring(TR) * RR_SLOT; }
 
-template <int DT, int EPI, int D, int LEAD = 3>
+// TC x (TR x 128) tiles: (256, 2) = cfg 27 (the 256 x 256 conv_glds2 tile, bitwise cfg 21), (64, 4) = cfg 28 (the
+// 64 x 512 tile of cfg 23, bitwise cfg 23: 8 waves of 64 channels x 64 pixels, two per tile row).  A 4-row tile's
+// chunk needs 4 + 2 * dil rows and its rows 2, 3 stay live to the chunk's last tap, so it runs 8 slots and issues a
+// row 2 stages ahead with a full drain per stage (LEAD = 2); the 2-row tile runs 4 slots, LEAD 3 or 4, counted waits.
+template <int DT, int EPI, int D, int LEAD = 3, int TC = 256, int TR = 2>
 __global__ void __launch_bounds__(512, 1) conv_rring_kernel(ConvArgs2 a) {
-  static_assert(LEAD >= 3 && LEAD <= 4, "row lead: >= 3 (the counted barrier wait leaves the last rows in flight), <= 4 (4 ring slots)");
+  static_assert((TC == 256 && TR == 2 && LEAD >= 3 && LEAD <= 4) || (TC == 64 && TR == 4 && LEAD == 2),
+                "row-ring configs: 256 x (2 x 128) with a 3- or 4-stage row lead (counted barrier waits need >= 3, 4 slots "
+                "allow <= 4); 64 x (4 x 128) with a 2-stage lead and a full drain");
   static_assert(D == 1 || D == 2, "dilation 1 or 2");
   static_assert(EPI != EPI_POOLFWD && EPI != EPI_CTXF && EPI != EPI_CTXB, "row-ring epilogues");
-  constexpr int WC = 4, NW = 8, TC = 256;
+  constexpr int NW = 8, WC = TC / 64, WP = NW / WC;
+  constexpr int TP = 128 * TR, PW = TP / (64 * WP);  // pixel fragments per wave / 4
+  constexpr int WPR = WP / TR;                       // waves per tile row
   constexpr int A_BYTES = TC * 128;
-  constexpr int GA = A_BYTES / 1024 / NW;         // 4 weight pieces per wave per stage (one per MFMA group)
-  constexpr int NR = 2 + 2 * D;                   // input rows of a 2-row tile per channel chunk
-  static_assert(GA == 4, "one weight piece per MFMA group");
+  constexpr int GA = A_BYTES / 1024 / NW;            // weight pieces per wave per stage (4 or 1)
+  constexpr int NR = TR + 2 * D;                     // input rows of a tile per channel chunk
+  constexpr int RING = rr_ring(TR);
+  static_assert(PW >= 1 && WPR >= 1 && (GA == 4 || GA == 1), "row-ring tile");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* ring = smem + 2 * A_BYTES;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wc = wave % WC, wp = wave / WC;       // wp = the tile row this wave computes
+  const int wc = wave % WC, wp = wave / WC;
+  const int rt = wp / WPR;                           // the tile row this wave computes
+  const int cbw = (wp - rt * WPR) * 64 * PW;         // and its first column in the tile
 
   const int tx = a.W >> 7;
   const int nct = a.Cout / TC;
-  const int npt = a.M >> 8;
+  const int npt = a.M / TP;
   const int tile = xcd_remap(blockIdx.x, nct * npt);
   const int ct = tile % nct, pt = tile / nct;
   const int q = pt / tx, cb = pt - q * tx;
-  const int grow0 = 2 * q;                                    // n * H + oh0
+  const int grow0 = TR * q;                                   // n * H + oh0
   const int oh0 = grow0 - (int)fdiv((uint32_t)grow0, a.fdH) * a.H;
   const int col0 = cb * 128;
   const int Ktot = 9 * a.Cin;
@@ -1241,37 +1260,46 @@ __global__ void __launch_bounds__(512, 1) conv_rring_kernel(ConvArgs2 a) {
   const int boff = (lane >> 3) * a.Cin + lc8;                 // lane's pixel / chunk inside a row piece
 
   if (tx == 1) {
-    // the guards of a one-block-wide map are always zero padding: written once (4 slots x 16 pixels x 8 chunks)
-    const int sl = tid >> 7, g = (tid >> 3) & 15;
-    reinterpret_cast<uint4*>(ring + sl * RR_SLOT + ((g < 8) ? g : 128 + g) * 128)[tid & 7] = make_uint4(0u, 0u, 0u, 0u);
+    // the guards of a one-block-wide map are always zero padding: written once (slots x 16 pixels x 8 chunks)
+    for (int e = tid; e < RING * 128; e += NW * 64) {
+      const int sl = e >> 7, g = (e >> 3) & 15;
+      reinterpret_cast<uint4*>(ring + sl * RR_SLOT + ((g < 8) ? g : 128 + g) * 128)[e & 7] = make_uint4(0u, 0u, 0u, 0u);
+    }
   }
 
   // stage s = 9 * chunk + tap (chunk-major, tap-minor: conv_glds2's k order).  The weights of stage s are issued two
   // stages ahead (in the stage-(s-2) MFMA gaps, like conv_glds2), the rows whose first tap is stage f LEAD stages
-  // ahead, after that stage's weights: the barrier wait before stage s + 1 then counts only the row pieces just
-  // issued (vmcnt retires in order), so a row has LEAD - 1 stages to arrive (a first-touch row comes from beyond
-  // L2; with LEAD = 2 and a full vmcnt drain per stage the kernel waited on them).  Row r of chunk c (input row
-  // oh0 - D + r) is first read by tap 0 (rows 0, 1), 3 (rows 2 .. 1 + D) or 6 (the rest) and last read by tap
-  // 3 * floor(r / D) + 2 (D = 1: rows 2, 3 both by tap 8): with 4 slots and LEAD <= 4 every slot's previous row
-  // has had its last tap at or before the issuing stage, whose fragments are in registers once its barrier passed.
+  // ahead, after that stage's weights: with LEAD >= 3 the barrier wait before stage s + 1 counts only the row pieces
+  // just issued (vmcnt retires in order), so a row has LEAD - 1 stages to arrive (a first-touch row comes from beyond
+  // L2; with LEAD = 2 and a full vmcnt drain per stage the 2-row kernel waited on them).  Row r of chunk c (input row
+  // oh0 - D + r) is first read by tap 0 (rows 0 .. TR - 1), 3 (the next D) or 6 (the last D) and last read by the
+  // last tap of the highest kh whose window holds it; with the ring sizes above every slot's previous row has had its
+  // last tap at or before the issuing stage, whose fragments are in registers once its barrier passed.
   auto issue_A = [&](int st, int buf, int p) {
+#if defined(CAN_PROBE) && CAN_PROBE == 5
+    return;                                  // diagnostic build (scripts/probe): no weight DMA in the row ring
+#endif
     const int c = st / 9, tap = st - 9 * c;
     glds16((const void*)(a.w + aoff[p] + tap * a.Cin + c * 64), lds_addr(smem + buf * A_BYTES + (wave + NW * p) * 1024));
   };
+  auto rows_at = [&](int tap) -> int { return (tap == 0) ? TR : (tap == 3 || tap == 6) ? D : 0; };
   // row pieces this wave issues for the rows first read by stage f (0 when f is past the end)
   auto row_pieces = [&](int f) -> int {
     const int c = f / 9, tap = f - 9 * c;
-    const int nr = (c >= nc) ? 0 : (tap == 0) ? 2 : (tap == 3 || tap == 6) ? D : 0;
+    const int nr = (c >= nc) ? 0 : rows_at(tap);
     return nr * (2 + ((tx > 1 && wave < 2) ? 1 : 0));
   };
   auto issue_rows = [&](int f) {
+#if defined(CAN_PROBE) && CAN_PROBE == 6
+    return;                                  // diagnostic build (scripts/probe): no row DMA in the row ring
+#endif
     const int c = f / 9, tap = f - 9 * c;
-    const int nr = (c >= nc) ? 0 : (tap == 0) ? 2 : (tap == 3 || tap == 6) ? D : 0;
+    const int nr = (c >= nc) ? 0 : rows_at(tap);
     for (int k = 0; k < nr; ++k) {
-      const int r = ((tap == 0) ? 0 : (tap == 3) ? 2 : 2 + D) + k;
+      const int r = ((tap == 0) ? 0 : (tap == 3) ? TR : TR + D) + k;
       const int ih = oh0 - D + r;
       const bool rv = (unsigned)ih < (unsigned)a.H;
-      unsigned char* slot = ring + ((c * NR + r) & (RR_RING - 1)) * RR_SLOT;
+      unsigned char* slot = ring + ((c * NR + r) & (RING - 1)) * RR_SLOT;
       const size_t rbase = ((size_t)(grow0 - D + r) * a.W + col0) * a.Cin + c * 64;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -1301,14 +1329,14 @@ __global__ void __launch_bounds__(512, 1) conv_rring_kernel(ConvArgs2 a) {
     }
   };
 
-  f32x4 acc[4][8];
+  f32x4 acc[4][4 * PW];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 4 * PW; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fq = lane >> 4;
-  auto read = [&](int st, int kk, frag8_t (&af)[4], frag8_t (&bfr)[8]) {
+  auto read = [&](int st, int kk, frag8_t (&af)[4], frag8_t (&bfr)[4 * PW]) {
     const uint4* As = reinterpret_cast<const uint4*>(smem + (st & 1) * A_BYTES);
     const int chunk = kk * 4 + fq;
 #pragma unroll
@@ -1317,28 +1345,29 @@ __global__ void __launch_bounds__(512, 1) conv_rring_kernel(ConvArgs2 a) {
       af[j] = __builtin_bit_cast(frag8_t, As[row * 8 + swz(row, chunk)]);
     }
     const int c = st / 9, tap = st - 9 * c, kh = (tap * 11) >> 5, kw = tap - 3 * kh;
-    const int hp = 8 + fr + (kw - 1) * D;          // slot pixel of this lane's column in fragment 0
+    const int hp = 8 + cbw + fr + (kw - 1) * D;    // slot pixel of this lane's column in fragment 0
     const unsigned char* base =
-        ring + ((c * NR + kh * D + wp) & (RR_RING - 1)) * RR_SLOT + hp * 128 + ((chunk ^ (hp & 7)) << 4);
+        ring + ((c * NR + kh * D + rt) & (RING - 1)) * RR_SLOT + hp * 128 + ((chunk ^ (hp & 7)) << 4);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) bfr[i] = __builtin_bit_cast(frag8_t, *reinterpret_cast<const uint4*>(base + i * 2048));
+    for (int i = 0; i < 4 * PW; ++i)
+      bfr[i] = __builtin_bit_cast(frag8_t, *reinterpret_cast<const uint4*>(base + i * 2048));
   };
-  auto mma = [&](const frag8_t (&af)[4], const frag8_t (&bfr)[8], int i0, int i1) {
+  auto mma = [&](const frag8_t (&af)[4], const frag8_t (&bfr)[4 * PW], int i0, int i1) {
 #pragma unroll
     for (int i = i0; i < i1; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[j][i] = mfma16<DT>(af[j], bfr[i], acc[j][i]);
   };
 
-  frag8_t a0[4], b0[8], a1[4], b1[8];
+  frag8_t a0[4], b0[4 * PW], a1[4], b1[4 * PW];
   // prologue: every row first read before stage LEAD, the weights of stages 0 and 1, then a full drain
 #pragma unroll
   for (int f = 0; f < LEAD; ++f) issue_rows(f);
 #pragma unroll
-  for (int p = 0; p < 4; ++p) issue_A(0, 0, p);
+  for (int p = 0; p < GA; ++p) issue_A(0, 0, p);
   if (nk > 1) {
 #pragma unroll
-    for (int p = 0; p < 4; ++p) issue_A(1, 1, p);
+    for (int p = 0; p < GA; ++p) issue_A(1, 1, p);
   }
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   read(0, 0, a0, b0);
@@ -1348,24 +1377,35 @@ __global__ void __launch_bounds__(512, 1) conv_rring_kernel(ConvArgs2 a) {
     const int buf = s & 1;
     read(s, 1, a1, b1);
     __builtin_amdgcn_sched_barrier(0);
-    mma(a0, b0, 0, 8);
+    mma(a0, b0, 0, 4 * PW);
     // this wave's reads of stage s are in registers; stage s + 1 (weights, rows) has landed: everything but the
-    // row pieces issued last stage
+    // row pieces issued last stage (LEAD >= 3) / everything (LEAD = 2)
     __builtin_amdgcn_sched_barrier(0);
     wait_vm(rp_prev);
     __builtin_amdgcn_s_waitcnt(0xC07F);
     asm volatile("s_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     const bool more = s + 2 < nk;
+    constexpr int ord = CANNET_DMA_ORDER_CT;
+    // part p = weight piece p (GA = 4; GA = 1: the one piece in part 0), the rows after part 3, placed per
+    // CANNET_DMA_ORDER_CT (common.h)
+    auto part = [&](int p) {
+      if (more && p < GA) issue_A(s + 2, buf, p);
+      if (p == 3) {
+        issue_rows(s + LEAD);
+        rp_prev = (LEAD >= 3) ? row_pieces(s + LEAD) : 0;
+      }
+    };
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      if (more) issue_A(s + 2, buf, g);
-      if (g == 3) {
-        issue_rows(s + LEAD);
-        rp_prev = row_pieces(s + LEAD);
-      }
+      if (ord == 0) part(g);
       __builtin_amdgcn_sched_barrier(0);
-      mma(a1, b1, 2 * g, 2 * g + 2);
+      mma(a1, b1, g * PW, (g + 1) * PW);
+      __builtin_amdgcn_sched_barrier(0);
+      if (ord != 0 && (ord == 1 || g < 3)) {
+        part(g);
+        if (ord == 2 && g == 2) part(3);
+      }
       __builtin_amdgcn_sched_barrier(0);
       if (g == 1) read(s + 1, 0, a0, b0);
       __builtin_amdgcn_sched_barrier(0);
@@ -1373,15 +1413,20 @@ __global__ void __launch_bounds__(512, 1) conv_rring_kernel(ConvArgs2 a) {
     __builtin_amdgcn_s_waitcnt(0xC07F);
   }
   read(nk - 1, 1, a1, b1);
-  mma(a0, b0, 0, 8);
-  mma(a1, b1, 0, 8);
-  glds_epilogue<DT, WC, 2, 2, EPI, 1>(a, acc, ct, pt, wc, wp, fr, fq);
+  mma(a0, b0, 0, 4 * PW);
+  mma(a1, b1, 0, 4 * PW);
+  glds_epilogue<DT, WC, WP, PW, EPI, TR>(a, acc, ct, pt, wc, wp, fr, fq);
 }
 
-// the row-ring kernel applies: 3x3, dilation 1 / 2, W % 128 == 0, H even, Cout % 256 == 0
-static bool rring_ok(int H, int W, int Cin, int Cout, int ksize, int dil, int epi) {
-  return ksize == 3 && (dil == 1 || dil == 2) && W % 128 == 0 && H % 2 == 0 && Cout % 256 == 0 && Cin % 64 == 0 &&
-         epi != EPI_POOLFWD && epi != EPI_SIGMOID && epi != EPI_CTXF && epi != EPI_CTXB;
+// the row-ring kernel applies: 3x3, dilation 1 / 2, W % 128 == 0; Cout % 256 == 0 with H even (cfg 27) or Cout == 64
+// with H % 4 == 0 (cfg 28); 0 = not applicable
+static int rring_cfg(int H, int W, int Cin, int Cout, int ksize, int dil, int epi) {
+  if (ksize != 3 || (dil != 1 && dil != 2) || W % 128 || Cin % 64 || epi == EPI_POOLFWD || epi == EPI_SIGMOID ||
+      epi == EPI_CTXF || epi == EPI_CTXB)
+    return 0;
+  if (Cout % 256 == 0 && H % 2 == 0) return 27;
+  if (Cout == 64 && H % 4 == 0) return 28;
+  return 0;
 }
 // CANNET_RRING: 0 = off, 1 (default) = dilation-1 layers, 2 = every dilation.  Per layer at batch 8 x 768 x 1024
 // (profiles/r3/ab_rring.txt) -2..-6 % vs cfg 21 with the rows issued 3 stages ahead (issued 2 ahead with a full
@@ -1392,27 +1437,32 @@ static int rring_mode() {
   return e == nullptr ? 1 : atoi(e);
 }
 
+template <int DT, int EPI, int TC, int TR, int LEAD, int D>
+static int launch_rring_one(const ConvArgs2& a, hipStream_t s) {
+  auto kfn = conv_rring_kernel<DT, EPI, D, LEAD, TC, TR>;
+  static bool attr = false;
+  if (!attr) {
+    CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, rr_lds(TC, TR)));
+    attr = true;
+  }
+  hipLaunchKernelGGL(kfn, dim3((a.Cout / TC) * (a.M / (128 * TR))), dim3(512), rr_lds(TC, TR), s, a);
+  return (int)hipGetLastError();
+}
+
 template <int DT, int EPI>
-static int launch_rring(const ConvArgs2& a, hipStream_t s) {
+static int launch_rring(const ConvArgs2& a, hipStream_t s, int cfg) {
   if constexpr (EPI == EPI_POOLFWD || EPI == EPI_SIGMOID || EPI == EPI_CTXF || EPI == EPI_CTXB) {
     return -16;
   } else {
-    if (!rring_ok(a.H, a.W, a.Cin, a.Cout, a.ksize, a.dil, EPI)) return -16;
+    if (rring_cfg(a.H, a.W, a.Cin, a.Cout, a.ksize, a.dil, EPI) != cfg) return -16;
+    if (cfg == 28)
+      return a.dil == 1 ? launch_rring_one<DT, EPI, 64, 4, 2, 1>(a, s) : launch_rring_one<DT, EPI, 64, 4, 2, 2>(a, s);
     // CANNET_RRING_LEAD: stages a row is issued ahead of its first tap (3 or 4, default 3; per layer 3 measured
     // 0.4 % ahead of 4, profiles/r3/ab_rring.txt)
     const char* le = getenv("CANNET_RRING_LEAD");
-    const int lead = (le && atoi(le) == 4) ? 4 : 3;
-    auto kfn = (a.dil == 1) ? (lead == 4 ? conv_rring_kernel<DT, EPI, 1, 4> : conv_rring_kernel<DT, EPI, 1, 3>)
-                            : (lead == 4 ? conv_rring_kernel<DT, EPI, 2, 4> : conv_rring_kernel<DT, EPI, 2, 3>);
-    static const void* attr_done[4] = {};
-    const int ai = (a.dil - 1) * 2 + (lead == 4 ? 1 : 0);
-    if (attr_done[ai] != (const void*)kfn) {
-      CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, RR_LDS));
-      attr_done[ai] = (const void*)kfn;
-    }
-    const int nct = a.Cout / 256, npt = a.M >> 8;
-    hipLaunchKernelGGL(kfn, dim3(nct * npt), dim3(512), RR_LDS, s, a);
-    return (int)hipGetLastError();
+    const bool l4 = le && atoi(le) == 4;
+    if (a.dil == 1) return l4 ? launch_rring_one<DT, EPI, 256, 2, 4, 1>(a, s) : launch_rring_one<DT, EPI, 256, 2, 3, 1>(a, s);
+    return l4 ? launch_rring_one<DT, EPI, 256, 2, 4, 2>(a, s) : launch_rring_one<DT, EPI, 256, 2, 3, 2>(a, s);
   }
 }
 
@@ -2222,7 +2272,7 @@ static int glds_bpart_rows(int cfg, int M) {
   switch (cfg) {
     case 11: case 21: case 26: case 27: tp = 256; wp = 2; break;   // 256 ch x 256 px, 4 x 2 waves (26: 2 x 2)
     case 12: case 22: tp = 256; wp = 4; break;   // 128 x 256, 2 x 4
-    case 13: case 23: tp = 512; wp = 8; break;   // 64 x 512, 1 x 8
+    case 13: case 23: case 28: tp = 512; wp = 8; break;   // 64 x 512, 1 x 8
     case 25: tp = 512; wp = 4; break;            // 128 x 512, 2 x 4 (2 fragments per wave)
     default: return 0;
   }
@@ -2252,7 +2302,7 @@ static int dispatch_glds(const ConvArgs2& a, int tile_cfg, hipStream_t s, int nb
     case 23: return launch_glds2<DT, 1, 8, 1, EPI>(a, s, nb);
     case 25: if (a.Cout % 128) return -8; return launch_glds2<DT, 2, 4, 2, EPI>(a, s, nb);   // 128 x 512, 160 KB LDS
     case 26: if (a.Cout % 256) return -8; return launch_glds2<DT, 2, 2, 2, EPI, 8>(a, s, nb);  // 256 x 256, 4 waves
-    case 27: if (nb > 1) return -8; return launch_rring<DT, EPI>(a, s);                    // 256 x 256 row ring
+    case 27: case 28: if (nb > 1) return -8; return launch_rring<DT, EPI>(a, s, cfg);    // row ring
   }
   return -9;
 }
@@ -2337,7 +2387,7 @@ static int conv_igemm_impl(const void* x, const void* w, const float* bias, cons
     if (!b.zero) return -10;
     if (epi == EPI_POOLBWD) { b.mask = nullptr; b.pcodes = (const uint32_t*)mask; }   // mask = max-pool codes
     b.H = H; b.W = W; b.Cin = Cin; b.Cout = Cout; b.ksize = ksize; b.dil = dil; b.M = a.M;
-    if (tile_cfg == 0 && rring_mode() >= dil && rring_ok(H, W, Cin, Cout, ksize, dil, epi)) tile_cfg = 27;
+    if (tile_cfg == 0 && rring_mode() >= dil) tile_cfg = rring_cfg(H, W, Cin, Cout, ksize, dil, epi);
     if (bpart != nullptr) {
       const int rows = glds_bpart_rows(tile_cfg ? tile_cfg : glds_default_cfg(Cin, Cout, ksize), a.M);
       if (rows > 0 && rows <= bpart_cap) { b.bpart = bpart; if (bpart_rows) *bpart_rows = rows; }

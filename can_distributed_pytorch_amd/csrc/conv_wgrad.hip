@@ -716,11 +716,17 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
         const bool more = st + 2 < nstage;
         StageAddr sa;
         if (more) sa = stage_addr(st + 2, buf);
+        constexpr int ord = CANNET_DMA_ORDER_CT;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          if ((g * PARTS) % 4 == 0 && more) issue_part(sa, g * PARTS / 4, PARTS);
+          if (ord == 0 && more) issue_part(sa, g, PARTS);
           __builtin_amdgcn_sched_barrier(0);
           mma(a1, b1, g * KW, (g + 1) * KW);
+          __builtin_amdgcn_sched_barrier(0);
+          if (ord != 0 && more && (ord == 1 || g < 3)) {
+            issue_part(sa, g, PARTS);
+            if (ord == 2 && g == 2) issue_part(sa, 3, PARTS);
+          }
           __builtin_amdgcn_sched_barrier(0);
           if (g == 1) read(buf ^ 1, 0, a0, b0);
           __builtin_amdgcn_sched_barrier(0);

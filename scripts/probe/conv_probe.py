@@ -16,8 +16,9 @@ SHAPES = [("F9", 512, 512, 96, 128, 1), ("B1", 1024, 512, 96, 128, 2), ("F6", 25
 
 def main():
     libs = {}
-    for m in range(int(os.environ.get("PROBE_MODES", "4"))):
-        lib = ctypes.CDLL(os.path.join(os.environ.get("PROBE_DIR", os.path.join(ROOT, "build", "probe")), f"conv_probe{m}.so"))
+    for m in [int(v) for v in os.environ.get("PROBE_MODES", "0,1,2,3").split(",")]:
+        lib = ctypes.CDLL(os.path.join(os.environ.get("PROBE_DIR", os.path.join(ROOT, "build", "probe")),
+                                       os.environ.get("PROBE_PREFIX", "conv_probe") + f"{m}.so"))
         f = lib.can_conv_igemm
         f.restype = ctypes.c_int
         f.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int] * 11 + [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,

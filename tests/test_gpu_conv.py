@@ -567,10 +567,13 @@ def test_glds_four_wave_tiles_bitwise(n, h, w, ci, co, k, dil, dtype, monkeypatc
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("n,h,w,ci,co,dil", [(2, 8, 128, 256, 256, 1), (1, 12, 128, 1024, 512, 2),
                                              (1, 6, 256, 128, 256, 1), (2, 10, 384, 64, 256, 2),
-                                             (1, 4, 256, 512, 512, 2), (1, 2, 128, 192, 256, 1)])
+                                             (1, 4, 256, 512, 512, 2), (1, 2, 128, 192, 256, 1),
+                                             # cfg 28: 64-channel 4-row tiles (8 row slots, 2-stage lead)
+                                             (2, 8, 128, 128, 64, 1), (1, 8, 512, 128, 64, 1), (1, 4, 256, 256, 64, 2)])
 def test_row_ring_conv_bitwise(n, h, w, ci, co, dil, dtype, monkeypatch):
-    """Row-ring 3x3 conv (cfg 27: activation rows staged once per 64-channel chunk, taps read shifted windows of
-    the row slots) == the LDS-DMA 256 x 256 kernel (cfg 21, CANNET_RRING=0) bitwise for every epilogue it takes:
+    """Row-ring 3x3 conv (cfg 27 / 28: activation rows staged once per 64-channel chunk, taps read shifted windows
+    of the row slots) == the LDS-DMA kernel of the same tile (cfg 21 256 x 256 / cfg 23 64 x 512, CANNET_RRING=0)
+    bitwise for every epilogue it takes:
     bias + ReLU, plain, bias, ReLU-mask data gradient with bias partials, pool-backward data gradient, fp32 store;
     one- and multi-block-wide maps (zero guards / neighbour-pixel guards), dilation 1 and 2, top/bottom padding."""
     from can_distributed_pytorch_amd.ops import conv as C

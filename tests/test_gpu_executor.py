@@ -255,3 +255,29 @@ def test_rccl_comm_init_is_bounded_when_a_peer_never_joins():
     with pytest.raises(RuntimeError, match="timed out"):
         C.RcclComm(0, 2, uid, torch.cuda.current_device(), 3.0)
     assert time.perf_counter() - t0 < 60
+
+
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_native_stepper_row_ring_matches_per_tap_kernel(mode, monkeypatch):
+    """The row-ring conv (cfg 27: dilation-1 layers by default, every dilation with CANNET_RRING=2) trains exactly
+    like the per-tap LDS-DMA kernel (CANNET_RRING=0): 1 x 64 x 1024 puts conv3_x on a 2-block-wide 256-column map
+    (neighbour-pixel guards), conv4_x and the backend on a 1-block-wide 128-column map (zero guards).  Weights match
+    bit for bit after a step; biases to rounding (a 2-block-wide map groups the epilogue's bias partials by 2 x 128
+    tiles instead of 256-pixel runs)."""
+    from can_distributed_pytorch_amd.engine.native import NativeStepper
+    _, nat_a = _models(12)
+    nat_b = copy.deepcopy(nat_a)
+    x = torch.randn(1, 3, 64, 1024, device="cuda")
+    gt = torch.rand(1, 1, 8, 128, device="cuda")
+    monkeypatch.setenv("CANNET_RRING", "0")
+    a = NativeStepper("cuda", lr=1e-4, graph=False, model=nat_a)
+    a.step(x, gt)
+    monkeypatch.setenv("CANNET_RRING", mode)
+    b = NativeStepper("cuda", lr=1e-4, graph=False, model=nat_b)
+    b.step(x, gt)
+    torch.cuda.synchronize()
+    for (name, pa), pb in zip(nat_a.named_parameters(), nat_b.parameters()):
+        if name.endswith("bias"):
+            torch.testing.assert_close(pb, pa, rtol=1e-5, atol=1e-7, msg=name)
+        else:
+            assert torch.equal(pa, pb), name
