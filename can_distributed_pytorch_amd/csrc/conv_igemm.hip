@@ -1425,7 +1425,8 @@ static int rring_cfg(int H, int W, int Cin, int Cout, int ksize, int dil, int ep
       epi == EPI_CTXF || epi == EPI_CTXB)
     return 0;
   if (Cout % 256 == 0 && H % 2 == 0) return 27;
-  if (Cout == 64 && H % 4 == 0) return 28;
+  const char* e64 = getenv("CANNET_RRING64");          // cfg 28: opt-in (CANNET_RRING64=1) until measured
+  if (Cout == 64 && H % 4 == 0 && e64 != nullptr && e64[0] == '1') return 28;
   return 0;
 }
 // CANNET_RRING: 0 = off, 1 (default) = dilation-1 layers, 2 = every dilation.  Per layer at batch 8 x 768 x 1024

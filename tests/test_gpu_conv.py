@@ -607,6 +607,7 @@ def test_row_ring_conv_bitwise(n, h, w, ci, co, dil, dtype, monkeypatch):
     monkeypatch.setenv("CANNET_RRING", "0")
     ref = run()
     monkeypatch.setenv("CANNET_RRING", "2")          # every dilation
+    monkeypatch.setenv("CANNET_RRING64", "1")        # and the 64-channel 4-row tiles
     got = run()
     assert len(got) == len(ref)
     for i, (g, r) in enumerate(zip(got, ref)):

@@ -273,6 +273,7 @@ def test_native_stepper_row_ring_matches_per_tap_kernel(mode, monkeypatch):
     a = NativeStepper("cuda", lr=1e-4, graph=False, model=nat_a)
     a.step(x, gt)
     monkeypatch.setenv("CANNET_RRING", mode)
+    monkeypatch.setenv("CANNET_RRING64", "1")
     b = NativeStepper("cuda", lr=1e-4, graph=False, model=nat_b)
     b.step(x, gt)
     torch.cuda.synchronize()
