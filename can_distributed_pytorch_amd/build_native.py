@@ -72,7 +72,7 @@ def _compile(src: str, headers, verbose=False, asan: bool = False) -> str:
         return obj
     common = ["-O3", "-fPIC", "-std=c++17", f"-I{CSRC}", "-Wno-unused-result"]
     # CANNET_EXTRA_HIPFLAGS: extra defines for A/B variant builds (scripts/gpu/ab_variant_build.sh), e.g.
-    # -DCANNET_DMA_ORDER_CT=1
+    # -DCANNET_DMA_ORDER_WG=0
     common += os.environ.get("CANNET_EXTRA_HIPFLAGS", "").split()
     if src.endswith(".hip"):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-x", "hip", "-c", src, "-o", obj, "-munsafe-fp-atomics"] + common

@@ -207,11 +207,19 @@ __device__ __forceinline__ void load_w1_frags(const bf16_t* w1, frag8_t (&w1f)[2
                                                                                 kk * 32 + fq * 8));
 }
 
-// LDS-DMA part placement in the MFMA groups of a stage's second K half (conv_glds2, conv_rring, wgrad_glds2), a
-// compile-time switch for A/B builds (-DCANNET_DMA_ORDER_CT=n; a run-time switch pushed the 256 x 256 kernels into
-// scratch): 0 = part g before group g, 1 = part g after group g, 2 = parts 0 / 1 after groups 0 / 1, 2 + 3 after 2
-#ifndef CANNET_DMA_ORDER_CT
-#define CANNET_DMA_ORDER_CT 0
+// LDS-DMA part placement in the MFMA groups of a stage's second K half, per kernel family, compile-time (a run-time
+// switch pushed the 256 x 256 kernels into scratch; A/B builds: -D...=n, scripts/gpu/ab_variant_build.sh):
+// 0 = part g before group g, 1 = part g after group g, 2 = parts 0 / 1 after groups 0 / 1, parts 2 + 3 after group 2.
+// Per layer at batch 8 x 768 x 1024 (profiles/r3/ab_dma_order.txt): conv_glds2 best at 0 (1: +2..4 %), the row ring
+// at 1 (-2..3 %), the weight-gradient GEMM at 2 (-2..4 %).
+#ifndef CANNET_DMA_ORDER_CONV
+#define CANNET_DMA_ORDER_CONV 0
+#endif
+#ifndef CANNET_DMA_ORDER_RR
+#define CANNET_DMA_ORDER_RR 1
+#endif
+#ifndef CANNET_DMA_ORDER_WG
+#define CANNET_DMA_ORDER_WG 2
 #endif
 
 // ---------------------------------------------------------------------------

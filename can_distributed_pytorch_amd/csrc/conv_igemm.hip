@@ -1112,7 +1112,7 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
       // the four MFMA groups of the second K half, DMA parts of stage s+2 between them, the reads of stage
       // s+1's first half after the second group
       const bool more = s + 2 < nk;
-      constexpr int ord = CANNET_DMA_ORDER_CT;
+      constexpr int ord = CANNET_DMA_ORDER_CONV;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         if (ord == 0 && more) issue_part(buf, g);
@@ -1386,9 +1386,9 @@ __global__ void __launch_bounds__(512, 1) conv_rring_kernel(ConvArgs2 a) {
     asm volatile("s_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     const bool more = s + 2 < nk;
-    constexpr int ord = CANNET_DMA_ORDER_CT;
+    constexpr int ord = CANNET_DMA_ORDER_RR;
     // part p = weight piece p (GA = 4; GA = 1: the one piece in part 0), the rows after part 3, placed per
-    // CANNET_DMA_ORDER_CT (common.h)
+    // CANNET_DMA_ORDER_RR (common.h)
     auto part = [&](int p) {
       if (more && p < GA) issue_A(s + 2, buf, p);
       if (p == 3) {
@@ -1425,8 +1425,10 @@ static int rring_cfg(int H, int W, int Cin, int Cout, int ksize, int dil, int ep
       epi == EPI_CTXF || epi == EPI_CTXB)
     return 0;
   if (Cout % 256 == 0 && H % 2 == 0) return 27;
-  const char* e64 = getenv("CANNET_RRING64");          // cfg 28: opt-in (CANNET_RRING64=1) until measured
-  if (Cout == 64 && H % 4 == 0 && e64 != nullptr && e64[0] == '1') return 28;
+  // cfg 28 (CANNET_RRING64=0: off): conv2_1's data gradient 0.435 -> 0.347 ms isolated, step 487.3 -> 489.9 img/s
+  // (profiles/r3/ab_dma_order.txt)
+  const char* e64 = getenv("CANNET_RRING64");
+  if (Cout == 64 && H % 4 == 0 && (e64 == nullptr || e64[0] != '0')) return 28;
   return 0;
 }
 // CANNET_RRING: 0 = off, 1 (default) = dilation-1 layers, 2 = every dilation.  Per layer at batch 8 x 768 x 1024

@@ -716,7 +716,7 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
         const bool more = st + 2 < nstage;
         StageAddr sa;
         if (more) sa = stage_addr(st + 2, buf);
-        constexpr int ord = CANNET_DMA_ORDER_CT;
+        constexpr int ord = CANNET_DMA_ORDER_WG;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           if (ord == 0 && more) issue_part(sa, g, PARTS);

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build a variant of the CURRENT tree with extra hipcc defines into ab_<NAME>/ (self-contained package + scripts +
 # bench.py) so one GPU call can time several compile-time variants on the same box.  Run HERE (CPU):
-#   scripts/gpu/ab_variant_build.sh v1 "-DCANNET_DMA_ORDER_CT=1"
+#   scripts/gpu/ab_variant_build.sh v1 "-DCANNET_DMA_ORDER_RR=0 -DCANNET_DMA_ORDER_WG=0"
 # then e.g. `python ab_v1/scripts/bench_convs.py ...` / `python ab_v1/bench.py ...` on the box.
 set -e
 name=$1; flags=$2
