@@ -1216,7 +1216,7 @@ __host__ __device__ constexpr int rr_lds(int TC, int TR) { return 2 * TC * 128 +
 // row 2 stages ahead with a full drain per stage (LEAD = 2); the 2-row tile runs 4 slots, LEAD 3 or 4, counted waits.
 template <int DT, int EPI, int D, int LEAD = 3, int TC = 256, int TR = 2>
 __global__ void __launch_bounds__(512, 1) conv_rring_kernel(ConvArgs2 a) {
-  static_assert((TC == 256 && TR == 2 && LEAD >= 3 && LEAD <= 4) || (TC == 64 && TR == 4 && LEAD == 2),
+  static_assert(((TC == 256 || TC == 128) && TR == 2 && LEAD >= 3 && LEAD <= 4) || (TC == 64 && TR == 4 && LEAD == 2),
                 "row-ring configs: 256 x (2 x 128) with a 3- or 4-stage row lead (counted barrier waits need >= 3, 4 slots "
                 "allow <= 4); 64 x (4 x 128) with a 2-stage lead and a full drain");
   static_assert(D == 1 || D == 2, "dilation 1 or 2");
@@ -1228,7 +1228,7 @@ __global__ void __launch_bounds__(512, 1) conv_rring_kernel(ConvArgs2 a) {
   constexpr int GA = A_BYTES / 1024 / NW;            // weight pieces per wave per stage (4 or 1)
   constexpr int NR = TR + 2 * D;                     // input rows of a tile per channel chunk
   constexpr int RING = rr_ring(TR);
-  static_assert(PW >= 1 && WPR >= 1 && (GA == 4 || GA == 1), "row-ring tile");
+  static_assert(PW >= 1 && WPR >= 1 && (GA == 4 || GA == 2 || GA == 1), "row-ring tile");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* ring = smem + 2 * A_BYTES;
@@ -1387,7 +1387,7 @@ __global__ void __launch_bounds__(512, 1) conv_rring_kernel(ConvArgs2 a) {
     __builtin_amdgcn_sched_barrier(0);
     const bool more = s + 2 < nk;
     constexpr int ord = CANNET_DMA_ORDER_RR;
-    // part p = weight piece p (GA = 4; GA = 1: the one piece in part 0), the rows after part 3, placed per
+    // part p = weight piece p (GA = 4; GA = 2 / 1: parts 0 .. GA - 1), the rows after part 3, placed per
     // CANNET_DMA_ORDER_RR (common.h)
     auto part = [&](int p) {
       if (more && p < GA) issue_A(s + 2, buf, p);
@@ -1425,6 +1425,11 @@ static int rring_cfg(int H, int W, int Cin, int Cout, int ksize, int dil, int ep
       epi == EPI_CTXF || epi == EPI_CTXB)
     return 0;
   if (Cout % 256 == 0 && H % 2 == 0) return 27;
+  // cfg 29 (128 x (2 x 128), the wave tile of cfg 22): CANNET_RRING128=1 for the cfg-22 layers (K > 1152), =2 also
+  // for the cfg-25 ones (128 x 512 tiles, K <= 1152)
+  const char* e128 = getenv("CANNET_RRING128");
+  const int m128 = e128 ? atoi(e128) : 0;
+  if (Cout % 128 == 0 && Cout % 256 != 0 && H % 2 == 0 && m128 >= ((9 * Cin > 1152) ? 1 : 2)) return 29;
   // cfg 28 (CANNET_RRING64=0: off): conv2_1's data gradient 0.435 -> 0.347 ms isolated, step 487.3 -> 489.9 img/s
   // (profiles/r3/ab_dma_order.txt)
   const char* e64 = getenv("CANNET_RRING64");
@@ -1460,6 +1465,8 @@ static int launch_rring(const ConvArgs2& a, hipStream_t s, int cfg) {
     if (rring_cfg(a.H, a.W, a.Cin, a.Cout, a.ksize, a.dil, EPI) != cfg) return -16;
     if (cfg == 28)
       return a.dil == 1 ? launch_rring_one<DT, EPI, 64, 4, 2, 1>(a, s) : launch_rring_one<DT, EPI, 64, 4, 2, 2>(a, s);
+    if (cfg == 29)
+      return a.dil == 1 ? launch_rring_one<DT, EPI, 128, 2, 3, 1>(a, s) : launch_rring_one<DT, EPI, 128, 2, 3, 2>(a, s);
     // CANNET_RRING_LEAD: stages a row is issued ahead of its first tap (3 or 4, default 3; per layer 3 measured
     // 0.4 % ahead of 4, profiles/r3/ab_rring.txt)
     const char* le = getenv("CANNET_RRING_LEAD");
@@ -2274,7 +2281,7 @@ static int glds_bpart_rows(int cfg, int M) {
   int tp = 0, wp = 0;
   switch (cfg) {
     case 11: case 21: case 26: case 27: tp = 256; wp = 2; break;   // 256 ch x 256 px, 4 x 2 waves (26: 2 x 2)
-    case 12: case 22: tp = 256; wp = 4; break;   // 128 x 256, 2 x 4
+    case 12: case 22: case 29: tp = 256; wp = 4; break;   // 128 x 256, 2 x 4
     case 13: case 23: case 28: tp = 512; wp = 8; break;   // 64 x 512, 1 x 8
     case 25: tp = 512; wp = 4; break;            // 128 x 512, 2 x 4 (2 fragments per wave)
     default: return 0;
@@ -2305,7 +2312,7 @@ static int dispatch_glds(const ConvArgs2& a, int tile_cfg, hipStream_t s, int nb
     case 23: return launch_glds2<DT, 1, 8, 1, EPI>(a, s, nb);
     case 25: if (a.Cout % 128) return -8; return launch_glds2<DT, 2, 4, 2, EPI>(a, s, nb);   // 128 x 512, 160 KB LDS
     case 26: if (a.Cout % 256) return -8; return launch_glds2<DT, 2, 2, 2, EPI, 8>(a, s, nb);  // 256 x 256, 4 waves
-    case 27: case 28: if (nb > 1) return -8; return launch_rring<DT, EPI>(a, s, cfg);    // row ring
+    case 27: case 28: case 29: if (nb > 1) return -8; return launch_rring<DT, EPI>(a, s, cfg);    // row ring
   }
   return -9;
 }

@@ -116,7 +116,7 @@ def conv_igemm(x: torch.Tensor, wpack: torch.Tensor, bias: Optional[torch.Tensor
         _check_act(mask, "mask", dtype=dt)
     if epi == EPI_POOLBWD:
         _check_codes(mask, (n, h, w, co))
-        if first or tile not in (0, 21, 22, 23, 25, 27, 28):
+        if first or tile not in (0, 21, 22, 23, 25, 27, 28, 29):
             raise ValueError("EPI_POOLBWD runs on the LDS-DMA kernels only")
     if out is None:
         out = torch.empty(*oshape, dtype=dt, device=x.device)

@@ -569,7 +569,9 @@ def test_glds_four_wave_tiles_bitwise(n, h, w, ci, co, k, dil, dtype, monkeypatc
                                              (1, 6, 256, 128, 256, 1), (2, 10, 384, 64, 256, 2),
                                              (1, 4, 256, 512, 512, 2), (1, 2, 128, 192, 256, 1),
                                              # cfg 28: 64-channel 4-row tiles (8 row slots, 2-stage lead)
-                                             (2, 8, 128, 128, 64, 1), (1, 8, 512, 128, 64, 1), (1, 4, 256, 256, 64, 2)])
+                                             (2, 8, 128, 128, 64, 1), (1, 8, 512, 128, 64, 1), (1, 4, 256, 256, 64, 2),
+                                             # cfg 29: 128-channel 2-row tiles (the wave tile of cfg 22)
+                                             (2, 6, 128, 256, 128, 1), (1, 4, 256, 384, 128, 2)])
 def test_row_ring_conv_bitwise(n, h, w, ci, co, dil, dtype, monkeypatch):
     """Row-ring 3x3 conv (cfg 27 / 28: activation rows staged once per 64-channel chunk, taps read shifted windows
     of the row slots) == the LDS-DMA kernel of the same tile (cfg 21 256 x 256 / cfg 23 64 x 512, CANNET_RRING=0)
@@ -608,6 +610,7 @@ def test_row_ring_conv_bitwise(n, h, w, ci, co, dil, dtype, monkeypatch):
     ref = run()
     monkeypatch.setenv("CANNET_RRING", "2")          # every dilation
     monkeypatch.setenv("CANNET_RRING64", "1")        # and the 64-channel 4-row tiles
+    monkeypatch.setenv("CANNET_RRING128", "1")       # and the 128-channel 2-row tiles (K > 1152: cfg 22's layers)
     got = run()
     assert len(got) == len(ref)
     for i, (g, r) in enumerate(zip(got, ref)):
