@@ -1425,24 +1425,28 @@ static int rring_cfg(int H, int W, int Cin, int Cout, int ksize, int dil, int ep
       epi == EPI_CTXF || epi == EPI_CTXB)
     return 0;
   if (Cout % 256 == 0 && H % 2 == 0) return 27;
-  // cfg 29 (128 x (2 x 128), the wave tile of cfg 22): CANNET_RRING128=1 for the cfg-22 layers (K > 1152), =2 also
-  // for the cfg-25 ones (128 x 512 tiles, K <= 1152)
+  // cfg 29 (128 x (2 x 128), the wave tile of cfg 22): CANNET_RRING128=1 (default) for the dilation-1 cfg-22 layers
+  // (K > 1152: conv3_1's data gradient 0.270 -> 0.253 ms), =2 also for the cfg-25 ones (128 x 512 tiles, K <= 1152:
+  // conv2_2 +2 %), =3 also dilation 2 (backend.8 forward +10 %); 0 = off (profiles/r3/ab_rring128.txt)
   const char* e128 = getenv("CANNET_RRING128");
-  const int m128 = e128 ? atoi(e128) : 0;
-  if (Cout % 128 == 0 && Cout % 256 != 0 && H % 2 == 0 && m128 >= ((9 * Cin > 1152) ? 1 : 2)) return 29;
+  const int m128 = e128 ? atoi(e128) : 1;
+  if (Cout % 128 == 0 && Cout % 256 != 0 && H % 2 == 0 && m128 >= ((9 * Cin > 1152) ? 1 : 2) && (dil == 1 || m128 >= 3))
+    return 29;
   // cfg 28 (CANNET_RRING64=0: off): conv2_1's data gradient 0.435 -> 0.347 ms isolated, step 487.3 -> 489.9 img/s
   // (profiles/r3/ab_dma_order.txt)
   const char* e64 = getenv("CANNET_RRING64");
   if (Cout == 64 && H % 4 == 0 && (e64 == nullptr || e64[0] != '0')) return 28;
   return 0;
 }
-// CANNET_RRING: 0 = off, 1 (default) = dilation-1 layers, 2 = every dilation.  Per layer at batch 8 x 768 x 1024
+// CANNET_RRING: 0 = off, 1 = dilation-1 layers, 2 (default) = every dilation.  With the after-group DMA placement
+// (CANNET_DMA_ORDER_RR = 1) the dilation-2 layers gain too: step 497.0 -> 501.3 img/s (profiles/r3/ab_rring128.txt).
+// Before that placement, per layer at batch 8 x 768 x 1024
 // (profiles/r3/ab_rring.txt) -2..-6 % vs cfg 21 with the rows issued 3 stages ahead (issued 2 ahead with a full
 // DMA drain per stage: dilation 1 -1..-4 %, dilation 2 +1..+7 %); the step: off 482.6, dilation 1 485.4, every
 // dilation 484.9 img/s (medians of 4 interleaved rounds)
 static int rring_mode() {
   const char* e = getenv("CANNET_RRING");
-  return e == nullptr ? 1 : atoi(e);
+  return e == nullptr ? 2 : atoi(e);
 }
 
 template <int DT, int EPI, int TC, int TR, int LEAD, int D>
