@@ -610,7 +610,7 @@ def test_row_ring_conv_bitwise(n, h, w, ci, co, dil, dtype, monkeypatch):
     ref = run()
     monkeypatch.setenv("CANNET_RRING", "2")          # every dilation
     monkeypatch.setenv("CANNET_RRING64", "1")        # and the 64-channel 4-row tiles
-XX
+    monkeypatch.setenv("CANNET_RRING128", "3")       # and the 128-channel 2-row tiles (every K, every dilation)
     got = run()
     assert len(got) == len(ref)
     for i, (g, r) in enumerate(zip(got, ref)):
