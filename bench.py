@@ -15,6 +15,11 @@ Contract (driver): ``python bench.py --gpus N --steps K --warmup W``.
 W untimed steps, then exactly K timed steps bracketed by barrier +
 synchronize; the max over ranks is reported; rank 0 prints ONE JSON line.
 
+``--device cpu`` rehearses the same chain without a GPU (gloo, this framework's
+flat-arena data-parallel engine on the plain-ATen model, tiny default shape):
+``bench.py --device cpu --gpus 2`` goes launch_ranks -> torchrun -> rank main
+-> max-reduced JSON exactly as the driver's N-GPU run does (tests/test_bench_contract.py).
+
 Every timed step is a full training step: H2D-free synthetic batch already
 resident (data="synthetic"), forward, loss, backward, gradient all-reduce,
 optimizer step.  After the timed region (not timed): a few steps with
@@ -46,10 +51,14 @@ def parse(argv=None):
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--batch", type=int, default=8, help="per-GPU batch")
-    p.add_argument("--height", type=int, default=768)
-    p.add_argument("--width", type=int, default=1024)
-    p.add_argument("--impl", choices=["hip", "torch"], default=os.environ.get("CANNET_BENCH_IMPL", "hip"))
+    p.add_argument("--batch", type=int, default=None, help="per-GPU batch (default 8; cpu: 2)")
+    p.add_argument("--height", type=int, default=None, help="default 768 (cpu: 64)")
+    p.add_argument("--width", type=int, default=None, help="default 1024 (cpu: 64)")
+    p.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
+                   help="cpu: gloo rehearsal of the multi-rank chain (--impl arena by default)")
+    p.add_argument("--impl", choices=["hip", "torch", "arena"], default=None,
+                   help="hip: native kernels + RCCL reducer (cuda default); torch: stock PyTorch + DDP; "
+                        "arena: plain-ATen model + this framework's flat-arena bucketed reducer (cpu default)")
     p.add_argument("--dtype", choices=["bf16", "fp32", "fp16"], default="bf16")
     p.add_argument("--bucket-mb", type=float, default=25.0, help="gradient all-reduce bucket cap (MiB)")
     p.add_argument("--reducer", choices=["rccl", "torch"], default=os.environ.get("CANNET_REDUCER", "rccl"),
@@ -59,7 +68,48 @@ def parse(argv=None):
     p.add_argument("--comm-steps", type=int, default=3, help="extra untimed steps with all-reduce timing events")
     p.add_argument("--mode", choices=["train", "infer"], default="train",
                    help="train: the headline training step; infer: forward-only density estimation (serving)")
-    return p.parse_args(argv)
+    a = p.parse_args(argv)
+    cpu = a.device == "cpu"
+    if a.impl is None:
+        a.impl = "arena" if cpu else os.environ.get("CANNET_BENCH_IMPL", "hip")
+    if cpu and a.impl == "hip":
+        p.error("--impl hip needs --device cuda")
+    if cpu and a.dtype != "fp32":
+        a.dtype = "fp32"                       # the CPU rehearsal computes in fp32
+    a.batch = a.batch or (2 if cpu else 8)
+    a.height = a.height or (64 if cpu else 768)
+    a.width = a.width or (64 if cpu else 1024)
+    return a
+
+
+def visible_gpu_count() -> int:
+    """GPUs this process may use, counted WITHOUT initialising HIP (torch.cuda.device_count() can fall back to
+    hipGetDeviceCount, and a process that has touched the GPU must not start the rank processes).
+
+    KFD topology nodes with SIMDs are the GPUs; one counts only if its render node /dev/dri/renderD<minor> is
+    accessible (a container sees only the devices it was given), then ROCR_/HIP_/CUDA_VISIBLE_DEVICES narrow it."""
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    n = 0
+    try:
+        nodes = os.listdir(base)
+    except OSError:
+        nodes = []
+    for node in nodes:
+        try:
+            props = dict(line.split()[:2] for line in open(os.path.join(base, node, "properties")) if line.strip())
+        except (OSError, ValueError):
+            continue
+        if int(props.get("simd_count", "0")) <= 0:
+            continue                           # a CPU node
+        minor = props.get("drm_render_minor")
+        if minor is not None and not os.access(f"/dev/dri/renderD{minor}", os.R_OK | os.W_OK):
+            continue
+        n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
 
 
 def _free_port() -> int:
@@ -71,13 +121,14 @@ def _free_port() -> int:
 
 
 def launch_ranks(a) -> int:
-    """--gpus N without a launcher: spawn N ranks with torch.distributed.run (no GPU call in this process)."""
-    import torch
-    n_vis = torch.cuda.device_count()          # does not initialise the GPU
-    if n_vis < a.gpus:
-        print(f"bench.py: --gpus {a.gpus} requested but only {n_vis} GPU(s) visible; refusing to report a "
-              f"different node size", file=sys.stderr)
-        return 2
+    """--gpus N without a launcher: spawn N ranks with torch.distributed.run.  Nothing here touches the GPU (no torch
+    import even): the GPUs are counted from the KFD topology (visible_gpu_count)."""
+    if a.device == "cuda":
+        n_vis = visible_gpu_count()
+        if n_vis < a.gpus:
+            print(f"bench.py: --gpus {a.gpus} requested but only {n_vis} GPU(s) visible; refusing to report a "
+                  f"different node size", file=sys.stderr)
+            return 2
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ)
@@ -123,7 +174,7 @@ def infer(a, trainer, pool, sync_all, world, rank, local, dev) -> int:
                        "image_hw": [a.height, a.width], "impl": a.impl, "mode": "infer"},
             "count_first_image": float(et[0].sum())}), flush=True)
     if world > 1:
-        dist.barrier(device_ids=[local])
+        dist.barrier(**({} if cpu else {"device_ids": [local]}))
         dist.destroy_process_group()
     return 0
 
@@ -142,10 +193,16 @@ def main(argv=None) -> int:
 
     import torch
     import torch.distributed as dist
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    cpu = a.device == "cpu"
+    if cpu:
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        if world > 1:
+            dist.init_process_group("nccl", device_id=dev)
 
     from can_distributed_pytorch_amd.engine.trainer import build_trainer
     from can_distributed_pytorch_amd.data.synthetic import make_synthetic_batch, expected_flops_per_image
@@ -160,8 +217,9 @@ def main(argv=None) -> int:
 
     def sync_all():
         if world > 1:
-            dist.barrier(device_ids=[local])
-        torch.cuda.synchronize()
+            dist.barrier(**({} if cpu else {"device_ids": [local]}))
+        if not cpu:
+            torch.cuda.synchronize()
 
     if a.mode == "infer":
         return infer(a, trainer, pool, sync_all, world, rank, local, dev)
@@ -184,18 +242,29 @@ def main(argv=None) -> int:
     extra = {}
     red = getattr(trainer, "reducer", None)
     native = a.impl == "hip" and a.dtype != "fp32"       # hip + fp32 = split-bf16 convs under the torch step
-    if native:
+    if native or a.impl == "arena":
         extra["reducer"] = None if red is None else red.transport
-        extra["rccl_world"] = (red.comm.world if (red is not None and red.comm is not None) else
-                               (1 if red is None else None))
+        if native:
+            extra["rccl_world"] = (red.comm.world if (red is not None and red.comm is not None) else
+                                   (1 if red is None else None))
         extra["buckets_mib"] = None if red is None else [round(b.numel * 4 / 2 ** 20, 3) for b in red.buckets]
         if a.comm_steps > 0 and not a.graph:
             trainer.comm_timing = True
             for i in range(a.comm_steps):
                 trainer.step(*pool[i % len(pool)])
             trainer.comm_timing = False
-            ms_comm = trainer.exposed_comm_ms()
-            extra["exposed_allreduce_ms"] = None if ms_comm is None else round(ms_comm, 4)
+            if native:
+                ms_comm = trainer.exposed_comm_ms()
+                extra["exposed_allreduce_ms"] = None if ms_comm is None else round(ms_comm, 4)
+            # per-bucket all-reduce timeline of the last diagnostic step (ms after the backward started), max over
+            # ranks of the exposed tail: shows whether the all-reduce kernels got CUs while the backward ran
+            rep = trainer.comm_report()
+            if rep is not None:
+                ex_t = torch.tensor([rep["exposed_ms"]], dtype=torch.float64, device=dev)
+                if world > 1:
+                    dist.all_reduce(ex_t, op=dist.ReduceOp.MAX)
+                rep["exposed_ms_max_over_ranks"] = round(float(ex_t), 4)
+            extra["allreduce_timeline"] = rep
         sync_all()
         from can_distributed_pytorch_amd.parallel.consistency import check_replicas_consistent
         try:
@@ -203,11 +272,13 @@ def main(argv=None) -> int:
         except RuntimeError as e:
             extra["replicas_consistent"] = False
             print(f"bench.py: {e}", file=sys.stderr)
-    peak = torch.tensor([torch.cuda.max_memory_allocated(dev), torch.cuda.max_memory_reserved(dev)],
-                        device=dev, dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(peak, op=dist.ReduceOp.MAX)
-    extra["peak_hbm_gb"] = {"allocated": round(float(peak[0]) / 1e9, 3), "reserved": round(float(peak[1]) / 1e9, 3)}
+    if not cpu:
+        peak = torch.tensor([torch.cuda.max_memory_allocated(dev), torch.cuda.max_memory_reserved(dev)],
+                            device=dev, dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(peak, op=dist.ReduceOp.MAX)
+        extra["peak_hbm_gb"] = {"allocated": round(float(peak[0]) / 1e9, 3),
+                                "reserved": round(float(peak[1]) / 1e9, 3)}
 
     ms = 1000.0 * dt / a.steps
     imgs = a.batch * world * a.steps / dt
@@ -226,10 +297,11 @@ def main(argv=None) -> int:
             # stock stack measured on 1 GPU; for N GPUs it is credited with perfect (N x) scaling
             "vs_baseline": (round(imgs / (BASELINE_IMGS_PER_SEC * world), 4) if BASELINE_IMGS_PER_SEC else None),
             "dtype": a.dtype,
-            "data": "synthetic (random-init weights, synthetic 768x1024 crowd images + count-preserving 1/8 density maps)",
+            "data": f"synthetic (random-init weights, synthetic {a.height}x{a.width} crowd images + "
+                    f"count-preserving 1/8 density maps)",
             "config": {"model": "CANNet", "global_batch": a.batch * world, "per_gpu_batch": a.batch,
                        "image_hw": [a.height, a.width], "seq_len": None,
-                       "parallelism": f"dp{world}", "impl": a.impl,
+                       "parallelism": f"dp{world}", "impl": a.impl, "device": a.device,
                        "graph": bool(a.graph) and native, "bucket_mb": a.bucket_mb,
                        "optimizer": "SGD(m=0.95) fp32 master", "loss": "MSE(sum)"},
             "train_tflops_per_s": round(tflops, 2),
@@ -238,7 +310,7 @@ def main(argv=None) -> int:
         out.update(extra)
         print(json.dumps(out), flush=True)
     if world > 1:
-        dist.barrier(device_ids=[local])
+        dist.barrier(**({} if cpu else {"device_ids": [local]}))
         dist.destroy_process_group()
     return 0
 

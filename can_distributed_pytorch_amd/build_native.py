@@ -54,6 +54,39 @@ def asan_env(base=None) -> dict:
     return env
 
 
+def source_files():
+    """Every file the extension is built from (kernels, runtime, headers), sorted."""
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")) +
+                  glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(CSRC, "*.inc")))
+
+
+def source_hash(files=None) -> str:
+    """sha256 over (name, content) of the csrc/ sources: embedded in _C at build time and recomputed by
+    ops/_ext.py at import, so a binary that does not match the tree's sources fails loudly."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in (files if files is not None else source_files()):
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+def extra_flags():
+    # CANNET_EXTRA_HIPFLAGS: extra defines for A/B variant builds (scripts/gpu/ab_variant_build.sh), e.g.
+    # -DCANNET_DMA_ORDER_WG=0.  Objects of a flagged build live in their own directory (build/native_<hash>), so
+    # setting or clearing the variable never mixes variant objects into the default build.
+    return os.environ.get("CANNET_EXTRA_HIPFLAGS", "").split()
+
+
+def build_dir(asan: bool = False) -> str:
+    import hashlib
+    fl = extra_flags()
+    tag = ("_" + hashlib.sha256(" ".join(fl).encode()).hexdigest()[:10]) if fl else ""
+    return BUILD + tag + ("_asan" if asan else "")
+
+
 def _newer(src_files, target) -> bool:
     if not os.path.exists(target):
         return True
@@ -66,14 +99,12 @@ ASAN_HOST = ["-fsanitize=address", "-fno-omit-frame-pointer", "-g"]
 
 def _compile(src: str, headers, verbose=False, asan: bool = False) -> str:
     import pybind11
-    bdir = BUILD + ("_asan" if asan else "")
+    bdir = build_dir(asan)
     obj = os.path.join(bdir, os.path.basename(src) + ".o")
     if not _newer([src] + headers, obj):
         return obj
     common = ["-O3", "-fPIC", "-std=c++17", f"-I{CSRC}", "-Wno-unused-result"]
-    # CANNET_EXTRA_HIPFLAGS: extra defines for A/B variant builds (scripts/gpu/ab_variant_build.sh), e.g.
-    # -DCANNET_DMA_ORDER_WG=0
-    common += os.environ.get("CANNET_EXTRA_HIPFLAGS", "").split()
+    common += extra_flags()
     if src.endswith(".hip"):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-x", "hip", "-c", src, "-o", obj, "-munsafe-fp-atomics"] + common
         if asan:   # host half only: each -fsanitize right after -Xarch_host
@@ -92,10 +123,25 @@ def _compile(src: str, headers, verbose=False, asan: bool = False) -> str:
     return obj
 
 
+def _hash_unit(bdir: str) -> str:
+    """build/native*/src_hash.cpp: the source hash and build flags as C strings (rewritten only when they change)."""
+    path = os.path.join(bdir, "src_hash.cpp")
+    text = ('extern "C" const char* can_src_hash() { return "%s"; }\n'
+            'extern "C" const char* can_build_flags() { return "%s"; }\n'
+            % (source_hash(), " ".join(extra_flags()).replace("\\", "\\\\").replace('"', '\\"')))
+    old = open(path).read() if os.path.exists(path) else None
+    if old != text:
+        with open(path, "w") as f:
+            f.write(text)
+    return path
+
+
 def build(jobs: int = 8, verbose: bool = False, asan: bool = False) -> str:
-    os.makedirs(BUILD + ("_asan" if asan else ""), exist_ok=True)
+    bdir = build_dir(asan)
+    os.makedirs(bdir, exist_ok=True)
     headers = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(CSRC, "*.inc"))
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
+    srcs.append(_hash_unit(bdir))
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         objs = list(ex.map(lambda s: _compile(s, headers, verbose, asan), srcs))
     out = ext_path(asan)

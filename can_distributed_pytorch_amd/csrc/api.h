@@ -33,11 +33,6 @@ int can_conv_pool_fwd(const void* x, const void* w, const float* bias, void* y, 
 int can_conv_pool_tp(int Cin, int Cout, int ksize, int tile_cfg);
 
 // conv1_2 with conv1_1's output recomputed from the NHWC4 image (never stored)
-int can_conv_f1(const void* x, const void* w, const float* bias, const void* img, const void* w1, const float* b1,
-                void* y, int N, int H, int W, int epi, int dt, void* stream);
-int can_conv_wgrad_f1(const void* dy, const void* img, const void* w1, const float* b1, float* ws, float* wsb,
-                      float* dw, float* db, int N, int H, int W, int S, float beta, float scale, const float* dscale,
-                      int dt, void* stream);
 
 // conv1_2's data gradient with conv1_1's weight gradient fused (slabs [S][36][64] + [S][64]; returns S or < 0)
 int can_conv_ws64_dgrad_w1g(const void* dy, const void* w, const void* mask, const void* img, void* y, float* w1slab,

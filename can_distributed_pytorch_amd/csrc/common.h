@@ -1,6 +1,7 @@
 // Shared helpers for the gfx950 (CDNA4, MI355X) kernels of this framework.
 // Written for wave64 / MFMA / 160 KiB LDS; no CUDA shims, no dual paths.
 #pragma once
+#include "dispatch.h"
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <stdint.h>
@@ -171,42 +172,6 @@ __device__ __forceinline__ int perm_row(int rho) {
   return (rho & ~63) | (((rl >> 2) & 3) << 4) | ((rl >> 4) << 2) | (rl & 3);
 }
 
-// conv1_1 on MFMA for 16 pixels: lane (fr, fq) gets channels fq*16 + 4j + r (j, r < 4) of pixel fr
-// in acc[j][r] (same D layout as the halo kernels' accumulators: perm_row-packed A rows).  img4:
-// LDS image halo [rows][HCI] of 8-byte NHWC4 pixels; pixel fr's 3x3 window starts at pix0(fr).
-template <int DT>
-__device__ __forceinline__ void conv1_1_frag(const uint2* img4, int HCI, int pix0, const frag8_t (&w1f)[2][4],
-                                             f32x4 (&acc)[4], int fq) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    const int t0 = kk * 8 + fq * 2;                 // this lane's taps t0, t0 + 1 (k = tap*4 + c)
-    uint2 lo = make_uint2(0u, 0u), hi = make_uint2(0u, 0u);
-    if (t0 < 9) {
-      const int kh = (t0 * 11) >> 5, kw = t0 - kh * 3;
-      lo = img4[pix0 + kh * HCI + kw];
-    }
-    if (t0 + 1 < 9) {
-      const int kh = ((t0 + 1) * 11) >> 5, kw = t0 + 1 - kh * 3;
-      hi = img4[pix0 + kh * HCI + kw];
-    }
-    const frag8_t b = __builtin_bit_cast(frag8_t, make_uint4(lo.x, lo.y, hi.x, hi.y));
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] = mfma16<DT>(w1f[kk][j], b, acc[j]);
-  }
-}
-
-// A fragments of the packed first-layer weights (perm_row order), straight from global (8 KB, L2-hot)
-__device__ __forceinline__ void load_w1_frags(const bf16_t* w1, frag8_t (&w1f)[2][4], int fr, int fq) {
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      w1f[kk][j] = __builtin_bit_cast(frag8_t, *reinterpret_cast<const uint4*>(w1 + perm_row(j * 16 + fr) * 64 +
-                                                                                kk * 32 + fq * 8));
-}
-
 // LDS-DMA part placement in the MFMA groups of a stage's second K half, per kernel family, compile-time (a run-time
 // switch pushed the 256 x 256 kernels into scratch; A/B builds: -D...=n, scripts/gpu/ab_variant_build.sh):
 // 0 = part g before group g, 1 = part g after group g, 2 = parts 0 / 1 after groups 0 / 1, parts 2 + 3 after group 2.
@@ -231,6 +196,12 @@ __device__ __forceinline__ void load_w1_frags(const bf16_t* w1, frag8_t (&w1f)[2
 // every kernel using these orders it itself: a counted s_waitcnt vmcnt(N) and an s_barrier before the first
 // ds_read of the staged buffer (cdna_hip_programming.md: M0 is written and restored inside the statement).
 // lds: the wave-uniform LDS byte address of the 1-KiB destination (lane l writes lds + 16 l).
+// Invariants every caller keeps (nothing checks them at run time):
+//  * the destination is wave-uniform: lds_addr() takes lane 0's address (readfirstlane), so a lane-divergent
+//    destination would silently land at lane 0's; swizzled images are made by permuting the per-lane SOURCE;
+//  * the issuing waves retire their own DMA with a counted s_waitcnt vmcnt(N) and pass an s_barrier before any
+//    wave ds_reads the buffer (hipcc inserts no wait for asm DMA); tests/test_gpu_conv.py compares every LDS-DMA
+//    kernel against an fp32 reference at tight tolerance, which a missing wait fails.
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return __builtin_amdgcn_readfirstlane((unsigned)(size_t)(const __attribute__((address_space(3))) void*)p);
 }

@@ -961,7 +961,7 @@ extern "C" int can_ctx_gemm(int mode, const float* x, const float* y, const floa
   }
   const int M = (mode == 2) ? C : N * 36;
   hipStream_t s = (hipStream_t)stream;
-  if (C <= 512 && N * 36 <= 512 && getenv("CANNET_CTX_GEMM_V1") == nullptr) {
+  if (C <= 512 && N * 36 <= 512) {
     // matrix-core form (K <= 512 on both sides): 16 x 16 tiles, K split over 8 waves
     const dim3 grid(C / 16, (M + 15) / 16, 4);
     if (mode == 0) hipLaunchKernelGGL(ctx_mm_kernel<0>, grid, dim3(512), 0, s, a);

@@ -895,15 +895,12 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds_kernel(ConvArgs2 a)
 //    first half of stage s+1 is read (right after the barrier) while the
 //    second half's MFMAs run, so LDS read latency is never exposed at the
 //    head of an MFMA burst.
-// JW = 8 (cfg 26, CANNET_GLDS_W4=1): each wave owns 128 channels (8 A fragments) x 64*PW pixels, so a
-// 256 x 256 tile runs on 4 waves (one per SIMD, 256 fp32 accumulators in AGPRs) instead of 8: every B fragment
-// read from LDS feeds 8 MFMAs instead of 4 (LDS fragment bytes per FLOP -1/3); same LDS image, DMA and
-// epilogue, bitwise-equal results.  Measured 14-27 % SLOWER per layer (profiles/r3/ab_glds_four_wave.txt): with
-// one wave per SIMD nothing covers the DMA issue and the stage barrier, so the 8-wave layout stays the default.
+// (A 4-wave layout of 128-channel waves, 8 A fragments each, measured 14-27 % slower per layer and was removed:
+// with one wave per SIMD nothing covers the DMA issue and the stage barrier, profiles/r3/ab_glds_four_wave.txt.)
 // ===========================================================================
-template <int DT, int WC, int WP, int PW, int EPI, int JW = 4>
+template <int DT, int WC, int WP, int PW, int EPI>
 __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a) {
-  static_assert(JW == 4 || JW == 8, "channel fragments per wave");
+  constexpr int JW = 4;                           // 64-channel waves: 4 A fragments
   if (blockIdx.y) {                               // batched launch: item blockIdx.y
     a.x += blockIdx.y * a.xbs;
     a.w += blockIdx.y * a.wbs;
@@ -915,7 +912,7 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int NIA = A_BYTES / 1024, NIB = B_BYTES / 1024;
   constexpr int GA = NIA / NW, GB = NIB / NW;
-  constexpr int JH = JW / 4;                      // 64-channel halves per wave
+  constexpr int JH = 1;
   static_assert(NIA % NW == 0 && NIB % NW == 0, "instruction split");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1076,7 +1073,6 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
   // context epilogues: row tables beside the staging ring when the launch reserved room for them (a.cC flag bit),
   // visible after the first barrier below
   constexpr bool CTX = (EPI == EPI_CTXF || EPI == EPI_CTXB);
-  static_assert(!CTX || JW == 4, "context epilogues: 64-channel waves");
   constexpr int CTX_Q = CTX ? (5 * (EPI == EPI_CTXF ? 24 : 12) * ((EPI == EPI_CTXF ? TC / 4 : TC) / 4) + NW * 64 - 1) /
                                   (NW * 64)
                             : 1;
@@ -1163,15 +1159,13 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
     else ctxb_epilogue<DT, WC, WP, PW>(a, acc[0], tab, ct, pt, rlo, wc, wp, fr, fq);
     return;
   } else {
-    // a JW = 8 wave is two 64-channel waves of the WC * JH x WP layout to the shared epilogue
-#pragma unroll
-    for (int h = 0; h < JH; ++h) glds_epilogue<DT, WC * JH, WP, PW, EPI>(a, acc[h], ct, pt, wc * JH + h, wp, fr, fq);
+    glds_epilogue<DT, WC, WP, PW, EPI>(a, acc[0], ct, pt, wc, wp, fr, fq);
   }
 }
 
-template <int DT, int WC, int WP, int PW, int EPI, int JW = 4>
+template <int DT, int WC, int WP, int PW, int EPI>
 static int launch_glds2(const ConvArgs2& a, hipStream_t s, int nb = 1) {
-  constexpr int TC = 16 * JW * WC, TP = 64 * PW * WP;
+  constexpr int TC = 64 * WC, TP = 64 * PW * WP;
   size_t lds = 2 * (size_t)(TC + TP) * 128;
   ConvArgs2 b = a;
   if (EPI == EPI_CTXF || EPI == EPI_CTXB) {
@@ -1181,7 +1175,7 @@ static int launch_glds2(const ConvArgs2& a, hipStream_t s, int nb = 1) {
     if (b.ctx_prologue) lds += tab;
     else if ((size_t)ctx_tab_row_bytes(EPI, TC) * ctx_max_rows(TP, a.W) > lds) return -15;
   }
-  auto kfn = conv_glds2_kernel<DT, WC, WP, PW, EPI, JW>;
+  auto kfn = conv_glds2_kernel<DT, WC, WP, PW, EPI>;
   static size_t attr_lds = 0;
   if (lds > attr_lds) {
     CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -1425,29 +1419,24 @@ static int rring_cfg(int H, int W, int Cin, int Cout, int ksize, int dil, int ep
       epi == EPI_CTXF || epi == EPI_CTXB)
     return 0;
   if (Cout % 256 == 0 && H % 2 == 0) return 27;
-  // cfg 29 (128 x (2 x 128), the wave tile of cfg 22): CANNET_RRING128=1 (default) for the dilation-1 cfg-22 layers
-  // (K > 1152: conv3_1's data gradient 0.270 -> 0.253 ms), =2 also for the cfg-25 ones (128 x 512 tiles, K <= 1152:
-  // conv2_2 +2 %), =3 also dilation 2 (backend.8 forward +10 %); 0 = off (profiles/r3/ab_rring128.txt)
-  const char* e128 = getenv("CANNET_RRING128");
-  const int m128 = e128 ? atoi(e128) : 1;
+  // cfg 29 (128 x (2 x 128), the wave tile of cfg 22): dispatch rring128 = 1 (default) for the dilation-1 cfg-22
+  // layers (K > 1152: conv3_1's data gradient 0.270 -> 0.253 ms), = 2 also for the cfg-25 ones (128 x 512 tiles,
+  // K <= 1152: conv2_2 +2 %), = 3 also dilation 2 (backend.8 forward +10 %); 0 = off (profiles/r3/ab_rring128.txt)
+  const int m128 = g_dispatch.rring128;
   if (Cout % 128 == 0 && Cout % 256 != 0 && H % 2 == 0 && m128 >= ((9 * Cin > 1152) ? 1 : 2) && (dil == 1 || m128 >= 3))
     return 29;
-  // cfg 28 (CANNET_RRING64=0: off): conv2_1's data gradient 0.435 -> 0.347 ms isolated, step 487.3 -> 489.9 img/s
-  // (profiles/r3/ab_dma_order.txt)
-  const char* e64 = getenv("CANNET_RRING64");
-  if (Cout == 64 && H % 4 == 0 && (e64 == nullptr || e64[0] != '0')) return 28;
+  // cfg 28 (dispatch rring64 = 0: off): conv2_1's data gradient 0.435 -> 0.347 ms isolated, step 487.3 -> 489.9
+  // img/s (profiles/r3/ab_dma_order.txt)
+  if (Cout == 64 && H % 4 == 0 && g_dispatch.rring64) return 28;
   return 0;
 }
-// CANNET_RRING: 0 = off, 1 = dilation-1 layers, 2 (default) = every dilation.  With the after-group DMA placement
+// dispatch rring: 0 = off, 1 = dilation-1 layers, 2 (default) = every dilation.  With the after-group DMA placement
 // (CANNET_DMA_ORDER_RR = 1) the dilation-2 layers gain too: step 497.0 -> 501.3 img/s (profiles/r3/ab_rring128.txt).
 // Before that placement, per layer at batch 8 x 768 x 1024
 // (profiles/r3/ab_rring.txt) -2..-6 % vs cfg 21 with the rows issued 3 stages ahead (issued 2 ahead with a full
 // DMA drain per stage: dilation 1 -1..-4 %, dilation 2 +1..+7 %); the step: off 482.6, dilation 1 485.4, every
 // dilation 484.9 img/s (medians of 4 interleaved rounds)
-static int rring_mode() {
-  const char* e = getenv("CANNET_RRING");
-  return e == nullptr ? 2 : atoi(e);
-}
+static int rring_mode() { return g_dispatch.rring; }
 
 template <int DT, int EPI, int TC, int TR, int LEAD, int D>
 static int launch_rring_one(const ConvArgs2& a, hipStream_t s) {
@@ -1471,12 +1460,9 @@ static int launch_rring(const ConvArgs2& a, hipStream_t s, int cfg) {
       return a.dil == 1 ? launch_rring_one<DT, EPI, 64, 4, 2, 1>(a, s) : launch_rring_one<DT, EPI, 64, 4, 2, 2>(a, s);
     if (cfg == 29)
       return a.dil == 1 ? launch_rring_one<DT, EPI, 128, 2, 3, 1>(a, s) : launch_rring_one<DT, EPI, 128, 2, 3, 2>(a, s);
-    // CANNET_RRING_LEAD: stages a row is issued ahead of its first tap (3 or 4, default 3; per layer 3 measured
-    // 0.4 % ahead of 4, profiles/r3/ab_rring.txt)
-    const char* le = getenv("CANNET_RRING_LEAD");
-    const bool l4 = le && atoi(le) == 4;
-    if (a.dil == 1) return l4 ? launch_rring_one<DT, EPI, 256, 2, 4, 1>(a, s) : launch_rring_one<DT, EPI, 256, 2, 3, 1>(a, s);
-    return l4 ? launch_rring_one<DT, EPI, 256, 2, 4, 2>(a, s) : launch_rring_one<DT, EPI, 256, 2, 3, 2>(a, s);
+    // rows are issued 3 stages ahead of their first tap (per layer 0.4 % ahead of 4, profiles/r3/ab_rring.txt)
+    if (a.dil == 1) return launch_rring_one<DT, EPI, 256, 2, 3, 1>(a, s);
+    return launch_rring_one<DT, EPI, 256, 2, 3, 2>(a, s);
   }
 }
 
@@ -1499,27 +1485,22 @@ struct HaloConvArgs {
   bf16_t* y;
   const bf16_t* zero;
   int N, H, W, tiles_x, tiles_y;
-  // F1 recompute (conv_halo64_kernel<.., F1 = 1>): the network input NHWC4 image and the
-  // first layer (packed [64][64], k = tap*4 + c; fp32 bias).  conv1_1's output
-  // X2 = relu(conv1_1(img)) is never stored: EPI_BIAS_RELU rebuilds the X2 halo from
-  // the image (x is ignored), EPI_MASK rebuilds the ReLU mask (X2 > 0) of its outputs.
+  // conv_ws64_kernel<.., EPI_MASK, W1G>: the NHWC4 network input
   const bf16_t* img = nullptr;
-  const bf16_t* w1 = nullptr;
-  const float* b1 = nullptr;
   // EPI_POOLFWD (CO = 64, TCOL = 64; H % 4 == 0, W % 64 == 0): the 2x2/s2 max-pool of the output tile
   // -> yp [N][H/2][W/2][64], its max-pool codes -> codes [N][H/2][W/2][8] (optional), y optional
   bf16_t* yp = nullptr;
   uint32_t* codes = nullptr;
-  // EPI_MASK (not F1): bias-gradient partials of the produced dY, [ntile * rows per tile][CO] fp32
+  // EPI_MASK: bias-gradient partials of the produced dY, [ntile * rows per tile][CO] fp32
   float* bpart = nullptr;
-  // conv_ws64_kernel<.., EPI_MASK, W1G>: conv1_1's weight gradient from the dY tile it just produced (img =
-  // the NHWC4 network input): per-block partial slabs w1slab [2 * grid][36][64] (k = tap*4 + c) and
+  // conv_ws64_kernel<.., EPI_MASK, W1G>: conv1_1's weight gradient from the dY tile it just produced (from
+  // img): per-block partial slabs w1slab [2 * grid][36][64] (k = tap*4 + c) and
   // w1bslab [2 * grid][64] (bias), reduced by the first-layer slab reduction; y may be null (dY not stored)
   float* w1slab = nullptr;
   float* w1bslab = nullptr;
 };
 
-template <int DT, int CO, int EPI, int TCOL, int F1 = 0>
+template <int DT, int CO, int EPI, int TCOL>
 __global__ void __launch_bounds__((CO == 64 && TCOL == 64) ? 256 : 512, (TCOL == 64) ? 2 : 1)
 conv_halo64_kernel(HaloConvArgs a) {
   constexpr int TR = 4, HR = TR + 2, HC = TCOL + 2;
@@ -1530,17 +1511,13 @@ conv_halo64_kernel(HaloConvArgs a) {
   constexpr int WTAP = CO * 128;                      // one tap of weights: CO rows x 64 ci
   constexpr int GW = WTAP / 1024 / NW;                // weight DMA pieces per wave per tap
   constexpr int PW = CO / 64;                         // pixel fragments per wave / 4
-  // F1: image halo of the X2 halo (fwd: (HR+2) x (HC+2)) or of the output tile (mask: HR x HC)
-  constexpr int IHR = (EPI == EPI_MASK) ? HR : HR + 2, IHC = (EPI == EPI_MASK) ? HC : HC + 2;
   static_assert(GW >= 1, "weights split");
   static_assert(TCOL == 128 || (TCOL == 64 && CO == 64), "tile");
-  static_assert(!F1 || (CO == 64 && (EPI == EPI_BIAS_RELU || EPI == EPI_MASK)), "F1 recompute: conv1_2 fwd/dgrad");
-  static_assert(EPI != EPI_POOLFWD || (CO == 64 && TCOL == 64 && !F1), "fused pool: conv1_2 64-column tiles");
+  static_assert(EPI != EPI_POOLFWD || (CO == 64 && TCOL == 64), "fused pool: conv1_2 64-column tiles");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* halo = smem;
   unsigned char* wring = smem + HALO_BYTES;
-  uint2* img4 = reinterpret_cast<uint2*>(wring + 3 * WTAP);   // F1 only: [IHR][IHC] image pixels
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
@@ -1551,42 +1528,15 @@ conv_halo64_kernel(HaloConvArgs a) {
   const int n = tile / (a.tiles_x * a.tiles_y);
   const int oh0 = ty * TR, ow0 = tx * TCOL;
 
-  // F1 forward: conv1_1's operands first, so the waits for them (vmcnt retires in issue order) never
-  // also wait for the weight-ring DMA issued below
-  frag8_t w1f[2][4];
-  float b1v[16];
-  if constexpr (F1 && EPI == EPI_BIAS_RELU) {
-    load_w1_frags(a.w1, w1f, lane & 15, lane >> 4);
-#pragma unroll
-    for (int c = 0; c < 16; c += 4) {
-      const float4 b4 = *reinterpret_cast<const float4*>(a.b1 + (lane >> 4) * 16 + c);
-      b1v[c] = b4.x; b1v[c + 1] = b4.y; b1v[c + 2] = b4.z; b1v[c + 3] = b4.w;
-    }
-  }
-  if constexpr (F1) {
-    // image pixels (8 B, NHWC4) of the region conv1_1 is recomputed on, zero outside the image
-    const int ir0 = (EPI == EPI_MASK) ? oh0 - 1 : oh0 - 2, ic0 = (EPI == EPI_MASK) ? ow0 - 1 : ow0 - 2;
-    const uint2* im = reinterpret_cast<const uint2*>(a.img);
-    for (int p = tid; p < IHR * IHC; p += NW * 64) {
-      const int rr = p / IHC, cc = p - rr * IHC;
-      const int ih = ir0 + rr, iw = ic0 + cc;
-      uint2 v = make_uint2(0u, 0u);
-      if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) v = im[(size_t)(n * a.H + ih) * a.W + iw];
-      img4[p] = v;
-    }
-    if constexpr (EPI == EPI_MASK) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read after the barriers
-  }
-  if constexpr (!F1 || EPI == EPI_MASK) {
-    // ---- halo DMA (once): piece i covers halo pixels 8i..8i+7
-    for (int i = wave; i < NHI; i += NW) {
-      const int hp = i * 8 + (lane >> 3);
-      const int hr = hp / HC, hc = hp - hr * HC;
-      const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
-      const void* src = a.zero;
-      if (hp < HPIX && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
-        src = a.x + ((size_t)(n * a.H + ih) * a.W + iw) * 64 + (((lane & 7) ^ (hc & 7)) * 8);
-      glds16(src, lds_addr((halo + i * 1024)));
-    }
+  // ---- halo DMA (once): piece i covers halo pixels 8i..8i+7
+  for (int i = wave; i < NHI; i += NW) {
+    const int hp = i * 8 + (lane >> 3);
+    const int hr = hp / HC, hc = hp - hr * HC;
+    const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
+    const void* src = a.zero;
+    if (hp < HPIX && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+      src = a.x + ((size_t)(n * a.H + ih) * a.W + iw) * 64 + (((lane & 7) ^ (hc & 7)) * 8);
+    glds16(src, lds_addr((halo + i * 1024)));
   }
   auto issue_w = [&](int t) {
     unsigned char* dst = wring + (t % 3) * WTAP;
@@ -1600,32 +1550,6 @@ conv_halo64_kernel(HaloConvArgs a) {
   issue_w(0);
   issue_w(1);
   const int fr = lane & 15, fq = lane >> 4;
-
-  if constexpr (F1 && EPI == EPI_BIAS_RELU) {
-    // X2 halo = relu(conv1_1(img) + b1) on MFMA, written in the DMA's layout (16-B channel chunk c of
-    // halo pixel (hr, hc) at chunk slot c ^ (hc & 7)); zero outside the image (conv1_2's padding)
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // image halo in LDS
-    for (int g = wave; g * 16 < HPIX; g += NW) {
-      const int hp = g * 16 + fr;
-      const int hpc = hp < HPIX ? hp : HPIX - 1;
-      const int hr = hpc / HC, hc = hpc - hr * HC;
-      f32x4 x2[4];
-      conv1_1_frag<DT>(img4, IHC, hr * IHC + hc, w1f, x2, fq);
-      const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
-      const bool inside = ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-      float v[16];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[j * 4 + q] = inside ? fmaxf(x2[j][q] + b1v[j * 4 + q], 0.f) : 0.f;
-      if (hp < HPIX) {
-        uint4* dst = reinterpret_cast<uint4*>(halo + hp * 128);
-        dst[(2 * fq) ^ (hc & 7)] = pack8h<DT>(v);
-        dst[(2 * fq + 1) ^ (hc & 7)] = pack8h<DT>(v + 8);
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // X2 halo stores done before the tap-0 barrier
-  }
 
   // wave -> (row, co half / column half)
   const int r = (NW == 4) ? wave : (wave >> 1);
@@ -1680,7 +1604,7 @@ conv_halo64_kernel(HaloConvArgs a) {
   // ---- epilogue: lane owns 16 consecutive channels of one pixel per fragment
   const int oh = oh0 + r;
   const int chb = wc * 64 + fq * 16;
-  constexpr bool BPART = (EPI == EPI_MASK && !F1);
+  constexpr bool BPART = (EPI == EPI_MASK);
   // bias partials: row = tile * (NW * 64 / CO) + this wave's (row, column-half) slot, written even by a
   // wave whose row is outside the image (zeros)
   float bs[16];
@@ -1700,36 +1624,16 @@ conv_halo64_kernel(HaloConvArgs a) {
     return;
   }
   float bias[16];
-  if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS || EPI == EPI_POOLFWD || (F1 && EPI == EPI_MASK)) {
-    const float* bsrc = (F1 && EPI == EPI_MASK) ? a.b1 : a.bias;   // F1 mask: conv1_1's bias
+  if (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS || EPI == EPI_POOLFWD) {
 #pragma unroll
     for (int c = 0; c < 16; c += 4) {
-      const float4 b4 = *reinterpret_cast<const float4*>(bsrc + chb + c);
+      const float4 b4 = *reinterpret_cast<const float4*>(a.bias + chb + c);
       bias[c] = b4.x; bias[c + 1] = b4.y; bias[c + 2] = b4.z; bias[c + 3] = b4.w;
     }
   }
-  if constexpr (F1 && EPI == EPI_MASK) load_w1_frags(a.w1, w1f, fr, fq);   // all DMA has retired here
 #pragma unroll
   for (int i = 0; i < 4 * PW; ++i) {
     const int ow = ow0 + colbase + i * 16 + fr;
-    if constexpr (F1 && EPI == EPI_MASK) {
-      // the ReLU mask of conv1_2's input, recomputed: X2 = relu(conv1_1(img) + b1) > 0 at (oh, ow)
-      f32x4 x2[4];
-      conv1_1_frag<DT>(img4, IHC, r * IHC + colbase + i * 16 + fr, w1f, x2, fq);
-      if (ow >= a.W) continue;
-      float v[16];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const bool pos = pos_bits(f2h<DT>(x2[j][q] + bias[j * 4 + q]));   // exactly the stored X2's sign
-          v[j * 4 + q] = pos ? acc[j][i][q] : 0.f;
-        }
-      const size_t off = ((size_t)(n * a.H + oh) * a.W + ow) * CO + chb;
-      *reinterpret_cast<uint4*>(a.y + off) = pack8h<DT>(v);
-      *reinterpret_cast<uint4*>(a.y + off + 8) = pack8h<DT>(v + 8);
-      continue;
-    }
     if (ow >= a.W) continue;
     float v[16];
 #pragma unroll
@@ -2139,8 +2043,8 @@ static int launch_ws64(const HaloConvArgs& a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-// ws64 (weight-stationary) instead of the halo kernel for Cin = Cout = 64 (CANNET_WS64=0: halo kernel)
-static bool use_ws64() { return getenv("CANNET_WS64") == nullptr || getenv("CANNET_WS64")[0] != '0'; }
+// ws64 (weight-stationary) instead of the halo kernel for Cin = Cout = 64 (dispatch ws64 = 0: halo kernel)
+static bool use_ws64() { return g_dispatch.ws64 != 0; }
 
 // ===========================================================================
 // First layer (conv1_1: 3 -> 64, 3x3, input NHWC4 bf16 = 8 B per pixel).
@@ -2236,13 +2140,12 @@ __global__ void __launch_bounds__(512) conv_first_halo_kernel(HaloConvArgs a) {
   }
 }
 
-template <int DT, int CO, int EPI, int TCOL, int F1 = 0>
+template <int DT, int CO, int EPI, int TCOL>
 static int launch_halo64(const HaloConvArgs& a, hipStream_t s) {
   constexpr int HALO_BYTES = ((6 * (TCOL + 2) + 7) / 8) * 1024;
   constexpr int NW = (CO == 64 && TCOL == 64) ? 4 : 8;
-  constexpr int IMG_BYTES = !F1 ? 0 : (EPI == EPI_MASK) ? 6 * (TCOL + 2) * 8 : 8 * (TCOL + 4) * 8;
-  const size_t lds = HALO_BYTES + 3 * (size_t)CO * 128 + IMG_BYTES;
-  auto kfn = conv_halo64_kernel<DT, CO, EPI, TCOL, F1>;
+  const size_t lds = HALO_BYTES + 3 * (size_t)CO * 128;
+  auto kfn = conv_halo64_kernel<DT, CO, EPI, TCOL>;
   static bool attr = false;
   if (!attr) {
     CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -2267,24 +2170,19 @@ static int launch_glds(const ConvArgs2& a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-// 256 x 256 tiles on 4 waves of 128 x 128 (cfg 26) instead of 8 waves of 64 x 128 (cfg 21); CANNET_GLDS_W4=1
-static bool glds_w4() {
-  const char* e = getenv("CANNET_GLDS_W4");
-  return e != nullptr && e[0] == '1';
-}
 // default LDS-DMA tile config: v2 (pipelined); 128 x 512 tiles measured faster for K <= 1152
 static int glds_default_cfg(int Cin, int Cout, int ksize) {
   const int ktot = ksize * ksize * Cin;
   return (Cout % 256 == 0) ? 21 : (Cout % 128 == 0) ? (ktot <= 1152 ? 25 : 22) : 23;
 }
 static int glds_cfg_tp(int cfg) {   // pixels per tile of a v2 config
-  return (cfg == 21 || cfg == 22 || cfg == 26) ? 256 : (cfg == 23 || cfg == 25) ? 512 : 0;
+  return (cfg == 21 || cfg == 22) ? 256 : (cfg == 23 || cfg == 25) ? 512 : 0;
 }
 // rows of the bias-partial matrix an LDS-DMA config writes: pixel tiles x waves along the pixels (0: none)
 static int glds_bpart_rows(int cfg, int M) {
   int tp = 0, wp = 0;
   switch (cfg) {
-    case 11: case 21: case 26: case 27: tp = 256; wp = 2; break;   // 256 ch x 256 px, 4 x 2 waves (26: 2 x 2)
+    case 11: case 21: case 27: tp = 256; wp = 2; break;   // 256 ch x 256 px, 4 x 2 waves
     case 12: case 22: case 29: tp = 256; wp = 4; break;   // 128 x 256, 2 x 4
     case 13: case 23: case 28: tp = 512; wp = 8; break;   // 64 x 512, 1 x 8
     case 25: tp = 512; wp = 4; break;            // 128 x 512, 2 x 4 (2 fragments per wave)
@@ -2296,10 +2194,7 @@ static int glds_bpart_rows(int cfg, int M) {
 template <int DT, int EPI>
 static int dispatch_glds(const ConvArgs2& a, int tile_cfg, hipStream_t s, int nb = 1) {
   int cfg = tile_cfg;
-  if (cfg == 0) {
-    cfg = glds_default_cfg(a.Cin, a.Cout, a.ksize);
-    if (cfg == 21 && glds_w4()) cfg = 26;
-  }
+  if (cfg == 0) cfg = glds_default_cfg(a.Cin, a.Cout, a.ksize);
   if constexpr (EPI == EPI_POOLFWD) {
     const int tp = glds_cfg_tp(cfg);
     if (tp == 0 || (a.H & 1) || a.W % (tp / 2) || a.yp == nullptr) return -12;
@@ -2315,7 +2210,6 @@ static int dispatch_glds(const ConvArgs2& a, int tile_cfg, hipStream_t s, int nb
     case 22: if (a.Cout % 128) return -8; return launch_glds2<DT, 2, 4, 1, EPI>(a, s, nb);
     case 23: return launch_glds2<DT, 1, 8, 1, EPI>(a, s, nb);
     case 25: if (a.Cout % 128) return -8; return launch_glds2<DT, 2, 4, 2, EPI>(a, s, nb);   // 128 x 512, 160 KB LDS
-    case 26: if (a.Cout % 256) return -8; return launch_glds2<DT, 2, 2, 2, EPI, 8>(a, s, nb);  // 256 x 256, 4 waves
     case 27: case 28: case 29: if (nb > 1) return -8; return launch_rring<DT, EPI>(a, s, cfg);    // row ring
   }
   return -9;
@@ -2347,7 +2241,7 @@ static int conv_igemm_impl(const void* x, const void* w, const float* bias, cons
   hipStream_t s = (hipStream_t)stream;
 #define CAN_EPI_CASE(L, E) \
   if (epi == E) return dispatch_tiles<DT, L, E>(a, tile_cfg, s);
-  const bool auto_halo = tile_cfg == 0 && getenv("CANNET_NO_HALO_CONV") == nullptr;
+  const bool auto_halo = tile_cfg == 0;
   if (first) {
     if ((tile_cfg == 32 || auto_halo) && Cout == 64 && epi == EPI_BIAS_RELU) {
       HaloConvArgs h;
@@ -2368,8 +2262,8 @@ static int conv_igemm_impl(const void* x, const void* w, const float* bias, cons
     HaloConvArgs h;
     h.x = a.x; h.w = a.w; h.bias = a.bias; h.mask = a.mask; h.y = a.y; h.zero = conv_zero_page();
     if (!h.zero) return -10;
-    // Cout = 64: 64-column tiles, two blocks per CU (CANNET_HALO_TCOL128 = the 128-column tiles)
-    const bool narrow = Cout == 64 && getenv("CANNET_HALO_TCOL128") == nullptr;
+    // Cout = 64: 64-column tiles, two blocks per CU
+    const bool narrow = Cout == 64;
     h.N = N; h.H = H; h.W = W; h.tiles_x = narrow ? (W + 63) / 64 : (W + 127) / 128; h.tiles_y = (H + 3) / 4;
     if (bpart != nullptr && epi == EPI_MASK) {
       const int rows_per_tile = (Cout == 128) ? 4 : narrow ? 4 : 8;   // NW * 64 / CO
@@ -2469,9 +2363,8 @@ static int conv_ctx_impl(int fwd, const void* x, const void* w, const float* tab
   b.fdW = make_fastdiv((uint32_t)W); b.fdH = make_fastdiv((uint32_t)H);
   b.ctab0 = tab0; b.ctab1 = tab1; b.cat = (bf16_t*)cat; b.cC = C;
   // tiles: 256 x 256 (8 waves, one block per CU) or 128 x 128 (4 waves, 64 KB ring: two blocks per CU, one block's
-  // epilogue beside the other's main loop); CANNET_CTX_TILE{F,B} = 256 / 128 overrides
-  const char* ev = getenv(fwd ? "CANNET_CTX_TILEF" : "CANNET_CTX_TILEB");
-  const int tile = ev ? atoi(ev) : 256;
+  // epilogue beside the other's main loop); dispatch ctx_tile_f / ctx_tile_b select
+  const int tile = fwd ? g_dispatch.ctx_tile_f : g_dispatch.ctx_tile_b;
   if (fwd) {
     b.mask = nullptr; b.fvp = (const bf16_t*)fv;
     return tile == 128 ? launch_glds2<DT, 2, 2, 1, EPI_CTXF>(b, s) : launch_glds2<DT, 4, 2, 2, EPI_CTXF>(b, s);
@@ -2508,22 +2401,6 @@ static int conv_pool_fwd_impl(const void* x, const void* w, const float* bias, v
   return dispatch_glds<DT, EPI_POOLFWD>(b, tile_cfg, s);
 }
 
-// conv1_2 with conv1_1 recomputed (its output never stored): epi EPI_BIAS_RELU = forward from the image,
-// EPI_MASK = data gradient (x = dY of conv1_2) with the ReLU mask of conv1_1 recomputed.
-template <int DT>
-static int conv_f1_impl(const void* x, const void* w, const float* bias, const void* img, const void* w1,
-                        const float* b1, void* y, int N, int H, int W, int epi, hipStream_t s) {
-  HaloConvArgs h;
-  h.x = (const bf16_t*)x; h.w = (const bf16_t*)w; h.bias = bias; h.mask = nullptr; h.y = (bf16_t*)y;
-  h.zero = conv_zero_page();
-  if (!h.zero) return -10;
-  h.img = (const bf16_t*)img; h.w1 = (const bf16_t*)w1; h.b1 = b1;
-  h.N = N; h.H = H; h.W = W; h.tiles_x = (W + 63) / 64; h.tiles_y = (H + 3) / 4;
-  if (epi == EPI_BIAS_RELU) return launch_halo64<DT, 64, EPI_BIAS_RELU, 64, 1>(h, s);
-  if (epi == EPI_MASK) return launch_halo64<DT, 64, EPI_MASK, 64, 1>(h, s);
-  return -6;
-}
-
 // conv1_2's data gradient (ws64, EPI_MASK: dX = relu-masked, mask = conv1_1's output) with conv1_1's weight
 // gradient accumulated from each produced tile (W1G); dX stored only when y is not null.  Writes 2 * grid slabs to
 // w1slab [S][36][64] / w1bslab [S][64]; returns S (> 0) or a negative error.
@@ -2552,11 +2429,6 @@ extern "C" int can_conv_ws64_dgrad_w1g(const void* dy, const void* w, const void
                                        void* stream) {
   CAN_DT_DISPATCH(dt, can::conv_ws64_dgrad_w1g_impl<DT>(dy, w, mask, img, y, w1slab, w1bslab, slab_cap, N, H, W,
                                                         (hipStream_t)stream));
-}
-
-extern "C" int can_conv_f1(const void* x, const void* w, const float* bias, const void* img, const void* w1,
-                           const float* b1, void* y, int N, int H, int W, int epi, int dt, void* stream) {
-  CAN_DT_DISPATCH(dt, can::conv_f1_impl<DT>(x, w, bias, img, w1, b1, y, N, H, W, epi, (hipStream_t)stream));
 }
 
 // dt: element type of x / w / mask / y (DT_BF16 = 0, DT_F16 = 1)

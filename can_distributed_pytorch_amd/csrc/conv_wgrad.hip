@@ -762,211 +762,6 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
     }
 }
 
-// ===========================================================================
-// v3 = v2's addressing (row-aligned stages, hoisted per-lane DMA offsets, dY
-// through a buffer resource) with a DEEPER ring: 32-pixel stages (one MFMA
-// K step) in an NBUF-deep LDS ring (32 KB per stage for 256 x 256 tiles),
-// NBUF stages issued ahead.  v2 keeps one 64-pixel stage in flight while it
-// computes the other (the DMA of stage s+2 has one stage of MFMA work,
-// ~2k cycles at full rate, to land: less than a loaded chip's LDS-DMA
-// latency, ~1.1 us; its waves sat 49 % of their cycles in s_waitcnt /
-// barrier waits, profiles/r2/pmc_conv_kernels.txt).  Here a stage issued in
-// iteration s is waited for in iteration s + NBUF - 1 (3-4 stages of MFMA
-// work later).  Per iteration: wait for stage s+1 -> barrier (stage s's
-// buffer is free: its fragments were read in iteration s-1) -> DMA of stage
-// s+NBUF into that buffer, one piece per group of 8 MFMAs, interleaved with
-// the 32 MFMAs of stage s and the fragment reads of stage s+1 (two register
-// sets).
-// ===========================================================================
-template <int DT, int WC, int WK, int KW, int NBUF>
-__global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds3_kernel(WgradArgs2 a) {
-  constexpr int NW = WC * WK;
-  constexpr int TCo = 64 * WC, TK = 64 * WK * KW;
-  constexpr int BKM = 32;                          // pixels per stage (one MFMA K step)
-  constexpr int RBA = TCo * 2, RBB = TK * 2;
-  constexpr int A_BYTES = BKM * RBA, B_BYTES = BKM * RBB;
-  constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int NIA = A_BYTES / 1024, NIB = B_BYTES / 1024;
-  constexpr int GA = NIA / NW, GB = NIB / NW;
-  constexpr int GP = GA + GB;                      // LDS-DMA pieces per wave per stage
-  static_assert(NIA % NW == 0 && NIB % NW == 0 && GA >= 1 && GB >= 1, "instruction split");
-  static_assert(RBB == 512 || RBB == 256, "B row = 256 or 128 k");
-  static_assert(NBUF >= 3, "ring depth");
-
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wc = wave % WC, wk = wave / WC;
-
-  const int nco = a.Cout / TCo, nkt = a.K / TK;
-  const int ntile = nco * nkt;
-  const int bid = xcd_remap(blockIdx.x, ntile * a.S * a.nb);
-  const int tile = bid % ntile, slice = (bid / ntile) % a.S, bt = bid / (ntile * a.S);
-  const int co0 = (tile % nco) * TCo, k0 = (tile / nco) * TK;
-  const int mbeg = slice * a.mslice;
-  const int mend = min(a.M, mbeg + a.mslice);
-  const int nstage = (mend > mbeg) ? (mend - mbeg) / BKM : 0;    // M, mslice multiples of 64
-  const bf16_t* gdy = a.dy + bt * a.dy_bs;
-  const bf16_t* gx = a.x + bt * a.x_bs;
-
-  const __amdgpu_buffer_rsrc_t dy_rsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)gdy, (short)0, a.M * a.Cout * 2, 0x00020000);
-  constexpr int ASTEP = NW * 1024 / RBA, BSTEP = NW * 1024 / RBB;    // rows between a wave's pieces
-  static_assert(GA == 1 || ASTEP % 16 == 0, "piece stride must keep the row swizzle");
-  static_assert(GB == 1 || BSTEP % 16 == 0, "piece stride must keep the row swizzle");
-  unsigned aoff0;
-  {
-    const int byte = wave * 1024 + lane * 16;
-    const int row = byte / RBA;
-    const int lc16 = swz8b<RBA>(row, ((byte % RBA) / 16) * 2) >> 1;
-    aoff0 = (unsigned)(row * a.Cout + co0 + lc16 * 8) * 2u;
-  }
-  const unsigned astride = (unsigned)(ASTEP * a.Cout * 2);
-  const int tap = k0 / a.Cin;
-  int dh = 0, dw = 0;
-  if (a.ksize == 3) {
-    const int kh = (tap * 11) >> 5;
-    dh = (kh - 1) * a.dil;
-    dw = (tap - kh * 3 - 1) * a.dil;
-  }
-  const int ci0 = k0 - tap * a.Cin;
-  int boff0, brow0;
-  {
-    const int byte = wave * 1024 + lane * 16;
-    const int row = byte / RBB;
-    brow0 = row;
-    const int lc16 = swz8b<RBB>(row, ((byte % RBB) / 16) * 2) >> 1;
-    boff0 = (row + dh * a.W + dw) * a.Cin + ci0 + lc16 * 8;
-  }
-  const int bstride = BSTEP * a.Cin;
-
-  struct StageAddr {
-    unsigned soff;
-    const bf16_t* xs;
-    int ow0;
-    bool row_ok;
-    unsigned char* sbase;
-  };
-  auto stage_addr = [&](int st) -> StageAddr {
-    StageAddr sa;
-    const int m0 = mbeg + st * BKM;
-    const uint32_t q = fdiv((uint32_t)m0, a.fdW);
-    sa.ow0 = m0 - (int)q * a.W;
-    const int oh = (int)q - (int)fdiv(q, a.fdH) * a.H;
-    sa.row_ok = (unsigned)(oh + dh) < (unsigned)a.H;
-    sa.sbase = smem + (st % NBUF) * STAGE;
-    sa.soff = (unsigned)m0 * (unsigned)a.Cout * 2u;
-    sa.xs = gx + (size_t)m0 * a.Cin;
-    return sa;
-  };
-  // piece pc of a stage: A pieces 0..GA-1, then B pieces
-  auto issue_piece = [&](const StageAddr& sa, int pc) {
-    if (pc < GA) {
-      const int j = pc;
-      blds16(dy_rsrc, aoff0 + j * astride, sa.soff, lds_addr(sa.sbase + (wave + NW * j) * 1024));
-    } else {
-      const int j = pc - GA;
-      const int iw = sa.ow0 + dw + brow0 + j * BSTEP;
-      const bool ok = sa.row_ok && ((unsigned)iw < (unsigned)a.W);
-      const void* src = ok ? (const void*)(sa.xs + boff0 + j * bstride) : (const void*)a.zero;
-      glds16(src, lds_addr(sa.sbase + A_BYTES + (wave + NW * j) * 1024));
-    }
-  };
-
-  f32x4 acc[4][4 * KW];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int i = 0; i < 4 * KW; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int g = lane >> 4, qd = (lane & 15) >> 2, p = lane & 3;
-  auto rd = [&](const unsigned char* base, int rb_wide, int rb, int col0) -> frag8_t {
-    const int r0 = 8 * g + qd;
-    const int c8 = (col0 >> 2) + p;
-    const int s0 = rb_wide ? swz8b<256>(r0, c8) : swz8b<128>(r0, c8);
-    const int s1 = rb_wide ? swz8b<256>(r0 + 4, c8) : swz8b<128>(r0 + 4, c8);
-    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + r0 * rb + s0 * 8));
-    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + (r0 + 4) * rb + s1 * 8));
-    typedef short s16x8 __attribute__((ext_vector_type(8)));
-    const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(frag8_t, v);
-  };
-  auto read = [&](int st, frag8_t (&af)[4], frag8_t (&bfr)[4 * KW]) {
-    const unsigned char* Ab = smem + (st % NBUF) * STAGE;
-    const unsigned char* Bb = Ab + A_BYTES;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) af[j] = rd(Ab, RBA >= 256, RBA, wc * 64 + j * 16);
-#pragma unroll
-    for (int i = 0; i < 4 * KW; ++i) bfr[i] = rd(Bb, RBB >= 256, RBB, wk * 64 * KW + i * 16);
-  };
-  auto mma = [&](const frag8_t (&af)[4], const frag8_t (&bfr)[4 * KW], int i0, int i1) {
-#pragma unroll
-    for (int i = i0; i < i1; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[j][i] = mfma16<DT>(af[j], bfr[i], acc[j][i]);
-  };
-
-  if (nstage > 0) {
-    // prologue: stages 0 .. NBUF-1 in flight, wait for stage 0
-#pragma unroll
-    for (int s = 0; s < NBUF; ++s)
-      if (s < nstage) {
-        const StageAddr sa = stage_addr(s);
-#pragma unroll
-        for (int pc = 0; pc < GP; ++pc) issue_piece(sa, pc);
-      }
-    if (nstage >= NBUF) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" :: "n"((NBUF - 1) * GP) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    frag8_t a0[4], b0[4 * KW], a1[4], b1[4 * KW];
-    read(0, a0, b0);
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    // steady state: every stage issued NBUF ahead; counted waits leave NBUF-2 stages in flight
-    auto body = [&](int st, frag8_t (&ac)[4], frag8_t (&bc)[4 * KW], frag8_t (&an)[4], frag8_t (&bn)[4 * KW]) {
-      // stage st+1 landed (this wave's pieces: all but the NBUF-2 younger stages), then every wave's
-      if (st + 1 < nstage) {
-        if (st + NBUF - 1 < nstage) asm volatile("s_waitcnt vmcnt(%0)" :: "n"((NBUF - 2) * GP) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      asm volatile("s_barrier" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      const bool more = st + NBUF < nstage;
-      StageAddr sa;
-      if (more) sa = stage_addr(st + NBUF);          // into stage st's buffer (its fragments are in ac / bc)
-      // 4 groups of MFMAs of stage st; DMA pieces of stage st+NBUF and the reads of stage st+1 between them
-#pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-#pragma unroll
-        for (int pc = gq * GP / 4; pc < (gq + 1) * GP / 4; ++pc)
-          if (more) issue_piece(sa, pc);
-        __builtin_amdgcn_sched_barrier(0);
-        mma(ac, bc, gq * KW, (gq + 1) * KW);
-        __builtin_amdgcn_sched_barrier(0);
-        if (gq == 0 && st + 1 < nstage) read(st + 1, an, bn);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      __builtin_amdgcn_s_waitcnt(0xC07F);          // lgkmcnt(0): stage st+1's fragments in registers
-    };
-    int st = 0;
-    for (; st + 1 < nstage; st += 2) {
-      body(st, a0, b0, a1, b1);
-      body(st + 1, a1, b1, a0, b0);
-    }
-    if (st < nstage) body(st, a0, b0, a1, b1);
-  }
-
-  const int fr = lane & 15, fq = lane >> 4;
-  float* slab = a.ws + ((size_t)bt * a.S + slice) * a.K * a.Cout;
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int i = 0; i < 4 * KW; ++i) {
-      const int k = k0 + wk * 64 * KW + i * 16 + fr;
-      const int co = co0 + wc * 64 + j * 16 + fq * 4;
-      *reinterpret_cast<f32x4*>(slab + (size_t)k * a.Cout + co) = acc[j][i];
-    }
-}
-
 // Bias gradient partials for the v2 path: part[b][co] = sum of dY rows of
 // chunk b (SB chunks, fixed order; wgrad_reduce sums the SB partials).  A
 // separate short launch with many blocks, so the GEMM grid stays whole rounds.
@@ -1020,21 +815,6 @@ __global__ void __launch_bounds__(256) bias_colsum_kernel(const bf16_t* __restri
   }
 }
 
-template <int DT, int WC, int WK, int KW, int NBUF>
-static int launch_wgrad4(const WgradArgs2& a, hipStream_t s) {
-  constexpr int STAGE = 32 * (64 * WC + 64 * WK * KW) * 2;
-  const size_t lds = (size_t)NBUF * STAGE;
-  auto kfn = wgrad_glds3_kernel<DT, WC, WK, KW, NBUF>;
-  static bool attr = false;
-  if (!attr) {
-    CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    attr = true;
-  }
-  const int ntile = (a.Cout / (64 * WC)) * (a.K / (64 * WK * KW));
-  hipLaunchKernelGGL(kfn, dim3(ntile * a.S * a.nb), dim3(64 * WC * WK), lds, s, a);
-  return (int)hipGetLastError();
-}
-
 template <int DT, int WC, int WK, int KW>
 static int launch_wgrad3(const WgradArgs2& a, hipStream_t s) {
   constexpr int STAGE = 64 * (64 * WC + 64 * WK * KW) * 2;
@@ -1071,14 +851,9 @@ struct HaloArgs {
   float* wsb;
   int N, H, W, Cin, Cout, K, S;
   int tiles_y, tiles_x, ntiles, tiles_per_slice;
-  // F1 (wgrad_halo_kernel<.., F1 = 1>, conv1_2): x is the NHWC4 network input and the layer input
-  // X2 = relu(conv1_1(x) + b1) is recomputed per stage from a 6 x 68 image halo (3.3 KB instead of
-  // the 33 KB X2 halo), so conv1_1's output is never stored.
-  const bf16_t* w1 = nullptr;
-  const float* b1 = nullptr;
 };
 
-template <int DT, int CO, int TH, int F1 = 0>
+template <int DT, int CO, int TH>
 __global__ void __launch_bounds__(576, 1) wgrad_halo_kernel(HaloArgs a) {
   constexpr int TW = 64;
   constexpr int HW_ = TW + 2;                       // halo width
@@ -1087,12 +862,10 @@ __global__ void __launch_bounds__(576, 1) wgrad_halo_kernel(HaloArgs a) {
   constexpr int RBD = CO * 2;                       // dY row bytes
   constexpr int DY_BYTES = NPIX * RBD;
   constexpr int X_BYTES = ((HH * HW_ * 128 + 1023) / 1024) * 1024;
-  constexpr int IMG_BYTES = F1 ? ((HH + 2) * (HW_ + 2) * 8 + 1023) / 1024 * 1024 : 0;   // F1: image halo
-  constexpr int STAGE = DY_BYTES + X_BYTES + IMG_BYTES;
+  constexpr int STAGE = DY_BYTES + X_BYTES;
   constexpr int NID = DY_BYTES / 1024;              // LDS-DMA instructions per stage
-  constexpr int NIX = F1 ? IMG_BYTES / 1024 : X_BYTES / 1024;
+  constexpr int NIX = X_BYTES / 1024;
   constexpr int NT = CO / 16;                       // co tiles of 16
-  static_assert(!F1 || CO == 64, "F1: conv1_2 (64 -> 64)");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1108,7 +881,7 @@ __global__ void __launch_bounds__(576, 1) wgrad_halo_kernel(HaloArgs a) {
   const int nstage = max(0, t_end - t_beg);
   const bool do_bias = (a.wsb != nullptr) && ci_t == 0 && wave == 4;
 
-  // i_lo .. i_hi: the stage's DMA pieces to issue (dY pieces [0, NID), X / image pieces [NID, NID + NIX))
+  // i_lo .. i_hi: the stage's DMA pieces to issue (dY pieces [0, NID), X pieces [NID, NID + NIX))
   auto issue = [&](int st, int buf, int i_lo = 0, int i_hi = -1) {
     if (i_hi < 0) i_hi = NID + NIX;
     const int t = t_beg + st;
@@ -1126,14 +899,6 @@ __global__ void __launch_bounds__(576, 1) wgrad_halo_kernel(HaloArgs a) {
         const int yy = y0 + p / TW, xx = x0 + p % TW;
         if (yy < a.H && xx < a.W) src = a.dy + ((size_t)(n * a.H + yy) * a.W + xx) * a.Cout + co0 + lc16 * 8;
         dst = sbase + i * 1024;
-      } else if constexpr (F1) {
-        // image halo rows y0-2 .. y0+TH+1, columns x0-2 .. x0+65, 2 pixels (16 B) per lane: x0 - 2 and
-        // W are even, so both pixels of a pair are inside or both outside the image
-        const int q2 = ((i - NID) * 1024 + lane * 16) / 8;   // first pixel of the pair
-        const int yy = y0 - 2 + q2 / (HW_ + 2), xx = x0 - 2 + q2 % (HW_ + 2);
-        if (q2 < (HH + 2) * (HW_ + 2) && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W)
-          src = a.x + ((size_t)(n * a.H + yy) * a.W + xx) * 4;
-        dst = sbase + DY_BYTES + X_BYTES + (i - NID) * 1024;
       } else {
         const int byte = (i - NID) * 1024 + lane * 16;
         const int q = byte / 128;
@@ -1146,67 +911,6 @@ __global__ void __launch_bounds__(576, 1) wgrad_halo_kernel(HaloArgs a) {
       glds16(src, lds_addr(dst));
     }
   };
-  // F1: X2 = relu(conv1_1(img) + b1) of the stage's (HH x HW_) halo into the X image, in the layout the
-  // DMA would have produced (16-B channel chunk c of row q at slot c ^ k2(q)); zero outside the image
-  // conv1_1's packed weights (8 KB) and bias live in LDS behind the two stage buffers and are re-read
-  // there every stage: 9 waves on 4 SIMDs leave no room to keep 48 more registers live across the
-  // stage loop, and a global (vmcnt-counted) reload inside the loop would wait for the next stage's
-  // DMA too (vmcnt retires in issue order)
-  unsigned char* w1s = smem + 2 * STAGE;
-  if constexpr (F1) {
-    for (int i = tid; i < 64 * 64 / 8; i += 576)
-      reinterpret_cast<uint4*>(w1s)[i] = reinterpret_cast<const uint4*>(a.w1)[i];
-    if (tid < 64) reinterpret_cast<float*>(w1s + 64 * 64 * 2)[tid] = a.b1[tid];
-  }
-  auto build_x2 = [&](int st, int buf) {
-    const int t = t_beg + st;
-    const int n = t / (a.tiles_y * a.tiles_x);
-    const int rem = t - n * a.tiles_y * a.tiles_x;
-    const int y0 = (rem / a.tiles_x) * TH, x0 = (rem % a.tiles_x) * TW;
-    unsigned char* Xb = smem + buf * STAGE + DY_BYTES;
-    const uint2* img4 = reinterpret_cast<const uint2*>(Xb + X_BYTES);
-    const int fr = lane & 15, fq = lane >> 4;
-    const bf16_t* w1l = reinterpret_cast<const bf16_t*>(w1s);
-    const float* b1s = reinterpret_cast<const float*>(w1s + 64 * 64 * 2);
-    for (int gidx = wave; gidx * 16 < HH * HW_; gidx += 9) {
-      const int qp = gidx * 16 + fr;
-      const int qc = qp < HH * HW_ ? qp : HH * HW_ - 1;
-      const int hr = qc / HW_, hc = qc - hr * HW_;
-      // im2col fragments of the pixel (taps t0, t0+1 of each K half), then one 16-channel tile at a
-      // time (few live registers: the 9-wave kernel sits at the 170-VGPR occupancy limit)
-      frag8_t bim[2];
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int t0 = kk * 8 + fq * 2;
-        uint2 lo = make_uint2(0u, 0u), hi = make_uint2(0u, 0u);
-        const int pix0 = hr * (HW_ + 2) + hc;
-        if (t0 < 9) lo = img4[pix0 + ((t0 * 11) >> 5) * (HW_ + 2) + t0 - ((t0 * 11) >> 5) * 3];
-        if (t0 + 1 < 9) hi = img4[pix0 + (((t0 + 1) * 11) >> 5) * (HW_ + 2) + t0 + 1 - (((t0 + 1) * 11) >> 5) * 3];
-        bim[kk] = __builtin_bit_cast(frag8_t, make_uint4(lo.x, lo.y, hi.x, hi.y));
-      }
-      const int yy = y0 - 1 + hr, xx = x0 - 1 + hc;
-      const bool inside = yy >= 0 && yy < a.H && xx >= 0 && xx < a.W && qp < HH * HW_;
-      const int k2 = ((((qp >> 1) & 1) | (((qp >> 3) & 1) << 1)) << 1);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        f32x4 x2 = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          const frag8_t wf = __builtin_bit_cast(
-              frag8_t, *reinterpret_cast<const uint4*>(w1l + perm_row(j * 16 + fr) * 64 + kk * 32 + fq * 8));
-          x2 = mfma16<DT>(wf, bim[kk], x2);
-        }
-        // channels fq*16 + 4j .. +3 of pixel qp: 8 bytes = half (j & 1) of 16-B chunk 2*fq + (j >> 1)
-        float v[4];
-#pragma unroll
-        for (int q4 = 0; q4 < 4; ++q4) v[q4] = inside ? fmaxf(x2[q4] + b1s[fq * 16 + j * 4 + q4], 0.f) : 0.f;
-        if (qp < HH * HW_)
-          *reinterpret_cast<uint2*>(Xb + qp * 128 + (((2 * fq + (j >> 1)) ^ k2) * 16) + (j & 1) * 8) =
-              make_uint2(pack2<DT>(v[0], v[1]), pack2<DT>(v[2], v[3]));
-      }
-    }
-  };
-
   f32x4 acc[NT][4];
   f32x4 accb[NT];
 #pragma unroll
@@ -1232,27 +936,10 @@ __global__ void __launch_bounds__(576, 1) wgrad_halo_kernel(HaloArgs a) {
   using RBdy = std::integral_constant<int, RBD>;
   using RBx = std::integral_constant<int, 128>;
 
-  if constexpr (F1) {
-    // software pipeline: the image halo runs two stages ahead of dY and X2(st + 1) is built in the same
-    // barrier phase as stage st's MFMAs, so one wave's build overlaps the other waves' matrix work.
-    // Buffer b = s & 1 holds dY(s), X2(s) and image(s) or image(s + 2) (image(s) is dead once X2(s) is
-    // built, one phase before image(s + 2) is issued into it)
-    if (nstage > 0) issue(0, 0);
-    if (nstage > 1) issue(1, 1, NID, NID + NIX);
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (nstage > 0) build_x2(0, 0);
-  } else {
-    if (nstage > 0) issue(0, 0);
-  }
+  if (nstage > 0) issue(0, 0);
   for (int st = 0; st < nstage; ++st) {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if constexpr (F1) {
-      if (st + 1 < nstage) issue(st + 1, (st + 1) & 1, 0, NID);
-      if (st + 2 < nstage) issue(st + 2, st & 1, NID, NID + NIX);
-      if (st + 1 < nstage) build_x2(st + 1, (st + 1) & 1);
-    } else {
-      if (st + 1 < nstage) issue(st + 1, (st + 1) & 1);
-    }
+    if (st + 1 < nstage) issue(st + 1, (st + 1) & 1);
     const unsigned char* Db = smem + (st & 1) * STAGE;
     const unsigned char* Xb = Db + DY_BYTES;
 #pragma unroll
@@ -1296,14 +983,13 @@ __global__ void __launch_bounds__(576, 1) wgrad_halo_kernel(HaloArgs a) {
   }
 }
 
-template <int DT, int CO, int TH, int F1 = 0>
+template <int DT, int CO, int TH>
 static int launch_halo(HaloArgs& a, hipStream_t s) {
   constexpr int TW = 64;
   constexpr int DY_BYTES = TH * TW * CO * 2;
   constexpr int X_BYTES = (((TH + 2) * (TW + 2) * 128 + 1023) / 1024) * 1024;
-  constexpr int IMG_BYTES = F1 ? ((TH + 4) * (TW + 4) * 8 + 1023) / 1024 * 1024 : 0;
-  const size_t lds = 2 * (size_t)(DY_BYTES + X_BYTES + IMG_BYTES) + (F1 ? 64 * 64 * 2 + 64 * 4 : 0);
-  auto kfn = wgrad_halo_kernel<DT, CO, TH, F1>;
+  const size_t lds = 2 * (size_t)(DY_BYTES + X_BYTES);
+  auto kfn = wgrad_halo_kernel<DT, CO, TH>;
   static bool attr = false;
   if (!attr) {
     CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -1524,8 +1210,7 @@ static int launch_reduce2(const float* ws, const float* wsb, float* dw, float* d
   const size_t plane = (size_t)K * Cout;
   const int nbias = (db != nullptr) ? (Cout + 15) / 16 : 0;
   auto grid = [&](int epb) { return (int)std::min<size_t>((plane + epb - 1) / epb, 4096) + nbias; };
-  const bool tiled_off = getenv("CANNET_REDUCE_GRIDSTRIDE") != nullptr;   // A/B switch, read per launch
-  if (!tiled_off && !first && taps == 9 && S <= 16 && Cout % 64 == 0 && Cin % RCI == 0 &&
+  if (g_dispatch.reduce_tiled && !first && taps == 9 && S <= 16 && Cout % 64 == 0 && Cin % RCI == 0 &&
       (Cout / 64) * (Cin / RCI) >= 256) {
     hipLaunchKernelGGL(wgrad_reduce_tiled_kernel, dim3((Cout / 64) * (Cin / RCI) + nbias), dim3(256), 0, s, ws, wsb,
                        dw, db, S, Sb, Cout, Cin, beta, scale, dscale);
@@ -1566,25 +1251,22 @@ static void wgrad_tile(int cfg, int* TCo, int* TK, int* BKM) {
 extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, int target_blocks, int* S_out,
                               int* mslice_out, int* cfg_out, int dil) {
   const int K = first ? 64 : ksize * ksize * Cin;
-  const char* force = getenv("CANNET_WGRAD_CFG");
   int cfg;
   // the halo weight-gradient kernel is dilation-1 only (B5: 256 -> 128, dil 2, reaches M >= 262144 at batch 32)
   const bool halo_ok = !first && ksize == 3 && dil == 1 && (Cout == 64 || Cout == 128) && Cin % 64 == 0;
   if (first) cfg = 0;
-  else if (halo_ok && getenv("CANNET_NO_HALO") == nullptr && M >= 262144) cfg = 8;
-  else if (Cout % 256 == 0 && K >= 2048) cfg = (K % 256 == 0 && getenv("CANNET_WGRAD_V1") == nullptr) ? 9 : 7;
-  else if (Cout % 256 == 0 && ksize == 1 && K % 256 == 0 && K >= 512 && getenv("CANNET_WGRAD_V1") == nullptr)
+  else if (halo_ok && M >= 262144) cfg = 8;
+  else if (Cout % 256 == 0 && K >= 2048) cfg = (K % 256 == 0) ? 9 : 7;
+  else if (Cout % 256 == 0 && ksize == 1 && K % 256 == 0 && K >= 512)
     cfg = 9;   // 1x1 with many output rows (the linearised context module's dW2cat: 2048 x 512)
   else if (Cout % 256 == 0 && K >= 1024)
-    cfg = (Cin % 128 == 0 && getenv("CANNET_WGRAD_V1") == nullptr && getenv("CANNET_WGRAD_NO_HALF") == nullptr) ? 10 : 2;
-  else if (Cout == 128 && Cin % 256 == 0 && K >= 2048 && getenv("CANNET_WGRAD_V1") == nullptr &&
-           getenv("CANNET_WGRAD_NO_HALF") == nullptr)
+    cfg = (Cin % 128 == 0) ? 10 : 2;
+  else if (Cout == 128 && Cin % 256 == 0 && K >= 2048)
     cfg = 11;
   else if (Cout % 128 == 0 && K >= 2048) cfg = 6;
   else if (Cout % 128 == 0) cfg = 1;
   else if (K >= 128) cfg = 3;
   else cfg = 4;
-  if (force && !first) cfg = atoi(force);
   int TCo, TK, BKM;
   wgrad_tile(cfg, &TCo, &TK, &BKM);
   if (cfg == 8) {
@@ -1599,7 +1281,7 @@ extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, in
   const int ntile = (Cout / TCo) * ((K + TK - 1) / TK);
   // whole rounds of co-resident blocks (no half-empty last round)
   int S = target_blocks / ntile;
-  if (cfg != 0 && cfg != 8 && getenv("CANNET_WGRAD_MANY_SLICES") == nullptr) {
+  if (cfg != 0 && cfg != 8) {
     // the pipelined kernels run one block per CU (LDS ring >= 128 KB): as few pixel slices as fill
     // whole rounds of the CUs to >= 90 % (fewer fp32 partial slabs to write and
     // reduce, longer K loops per block)
@@ -1624,14 +1306,6 @@ extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, in
   S = (M + mslice - 1) / mslice;
   *S_out = S; *mslice_out = mslice; *cfg_out = cfg;
   return 0;
-}
-
-// ring depth of the 256 x 256 weight-gradient GEMM (CANNET_WGRAD_RING: 0 = v2 two 64-pixel stages, 4 / 5 = v3
-// ring of 32-pixel stages)
-static int wgrad_ring_depth() {
-  const char* e = getenv("CANNET_WGRAD_RING");
-  const int d = e ? atoi(e) : 0;
-  return (d == 4 || d == 5) ? d : 0;
 }
 
 static const can::bf16_t* zero_page() {
@@ -1700,10 +1374,9 @@ static int conv_wgrad_impl(const void* dy, const void* x, float* ws, float* wsb,
       h.dy = a.dy; h.x = a.x; h.zero = a.zero; h.ws = ws; h.wsb = wsb_used;
       h.N = N; h.H = H; h.W = W; h.Cin = Cin; h.Cout = Cout; h.K = K; h.S = S;
       // Cout = 128 runs as two 64-channel co tiles.  Default: the row-ring kernel (4-row tiles walked
-      // down 64-column strips, each input row fetched once per strip); CANNET_WGRAD_RING=0: 2-row tiles
+      // down 64-column strips, each input row fetched once per strip); dispatch wgrad_halo_ring = 0: 2-row tiles
       // with a full halo per tile
-      const char* ring_env = getenv("CANNET_WGRAD_RING");
-      const bool ring = ring_env == nullptr || atoi(ring_env) != 0;
+      const bool ring = g_dispatch.wgrad_halo_ring != 0;
       const int th = ring ? 4 : 2;
       h.tiles_y = (H + th - 1) / th; h.tiles_x = (W + 63) / 64; h.ntiles = N * h.tiles_y * h.tiles_x;
       h.tiles_per_slice = (h.ntiles + S - 1) / S;
@@ -1731,10 +1404,7 @@ static int conv_wgrad_impl(const void* dy, const void* x, float* ws, float* wsb,
           }
           WgradArgs2 g = a;
           g.wsb = nullptr;
-          const int ring = wgrad_ring_depth();
-          if (ring == 5) rc = launch_wgrad4<DT, 4, 2, 2, 5>(g, s);
-          else if (ring == 4) rc = launch_wgrad4<DT, 4, 2, 2, 4>(g, s);
-          else rc = launch_wgrad3<DT, 4, 2, 2>(g, s);
+          rc = launch_wgrad3<DT, 4, 2, 2>(g, s);
         } else
           rc = launch_wgrad2<DT, 4, 2, 1, 2, 2, 2>(a, s);   // same tiles / slicing as cfg 7
         break;
@@ -1823,36 +1493,8 @@ extern "C" int can_conv_wgrad_1x1_batched(const void* dy, const void* x, float* 
                                                       mslice, beta, scale, dscale, (hipStream_t)stream));
 }
 
-// conv1_2 weight gradient with its input X2 = relu(conv1_1(img) + b1) recomputed from the NHWC4 image
-// (conv1_1's output is never stored).  dY [N,H,W,64], img [N,H,W,4], w1 packed [64][64], b1 fp32 [64].
-template <int DT>
-static int conv_wgrad_f1_impl(const void* dy, const void* img, const void* w1, const float* b1, float* ws, float* wsb,
-                              float* dw, float* db, int N, int H, int W, int S, float beta, float scale,
-                              const float* dscale, hipStream_t s) {
-  using namespace can;
-  if (W % 2 || S < 1) return -3;
-  HaloArgs h;
-  h.dy = (const bf16_t*)dy; h.x = (const bf16_t*)img; h.zero = zero_page(); h.ws = ws;
-  h.wsb = (db != nullptr) ? wsb : nullptr;
-  if (!h.zero) return -7;
-  h.N = N; h.H = H; h.W = W; h.Cin = 64; h.Cout = 64; h.K = 576; h.S = S;
-  h.tiles_y = (H + 1) / 2; h.tiles_x = (W + 63) / 64; h.ntiles = N * h.tiles_y * h.tiles_x;
-  h.tiles_per_slice = (h.ntiles + S - 1) / S;
-  h.w1 = (const bf16_t*)w1; h.b1 = b1;
-  int rc = launch_halo<DT, 64, 2, 1>(h, s);
-  if (rc) return rc;
-  return launch_reduce2(ws, h.wsb, dw, db, S, S, 576, 64, 64, 9, 0, beta, scale, dscale, s);
-}
-
 // first-layer slab reduction: ws [S][36][64] (k = tap*4 + c), wsb [S][64] -> dW [64][3][3][3], db [64]
 extern "C" int can_wgrad_reduce_first(const float* ws, const float* wsb, float* dw, float* db, int S, float beta,
                                       float scale, const float* dscale, void* stream) {
   return launch_reduce2(ws, wsb, dw, db, S, S, 36, 64, 4, 9, 1, beta, scale, dscale, (hipStream_t)stream);
-}
-
-extern "C" int can_conv_wgrad_f1(const void* dy, const void* img, const void* w1, const float* b1, float* ws,
-                                 float* wsb, float* dw, float* db, int N, int H, int W, int S, float beta, float scale,
-                                 const float* dscale, int dt, void* stream) {
-  CAN_DT_DISPATCH(dt, conv_wgrad_f1_impl<DT>(dy, img, w1, b1, ws, wsb, dw, db, N, H, W, S, beta, scale, dscale,
-                                             (hipStream_t)stream));
 }

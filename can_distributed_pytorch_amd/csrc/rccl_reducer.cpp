@@ -40,6 +40,8 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <tuple>
+#include <utility>
 #include <vector>
 
 namespace py = pybind11;
@@ -84,8 +86,9 @@ static ncclRedOp_t to_op(int code) {
 // polls the communicator until that completes (bounded too) before the next call.
 class RcclComm {
  public:
-  RcclComm(int rank, int world, const std::string& uid, int device, double init_timeout_s)
-      : rank_(rank), world_(world), device_(device), timeout_(init_timeout_s) {
+  RcclComm(int rank, int world, const std::string& uid, int device, double init_timeout_s,
+           double coll_timeout_s = 120.0)
+      : rank_(rank), world_(world), device_(device), timeout_(init_timeout_s), coll_timeout_(coll_timeout_s) {
     if (uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("bad ncclUniqueId size");
     ncclUniqueId id;
     memcpy(&id, uid.data(), sizeof(id));
@@ -99,20 +102,33 @@ class RcclComm {
       nccl_check(r, "ncclCommInitRankConfig");
     }
     try {
-      settle("ncclCommInitRankConfig");
+      settle("ncclCommInitRankConfig", timeout_);
     } catch (...) {
       if (comm_) ncclCommAbort(comm_);
       comm_ = nullptr;
       throw;
     }
   }
+  // Non-blocking communicator: finalize (flushes outstanding work) may return ncclInProgress, so it is settled with
+  // a bound before the destroy; a finalize that fails or does not settle in time aborts instead of hanging the
+  // process at exit.
   ~RcclComm() {
-    if (comm_) ncclCommDestroy(comm_);
+    if (!comm_) return;
+    try {
+      ncclResult_t r = ncclCommFinalize(comm_);
+      if (r == ncclInProgress) settle("ncclCommFinalize", coll_timeout_);
+      else nccl_check(r, "ncclCommFinalize");
+      ncclCommDestroy(comm_);
+    } catch (...) {
+      ncclCommAbort(comm_);
+    }
+    comm_ = nullptr;
   }
-  // Every RCCL call on this communicator goes through here: ncclInProgress is settled, anything else thrown.
+  // Every RCCL call on this communicator goes through here: ncclInProgress is settled (bounded by the collective
+  // timeout, much shorter than the init deadline), anything else thrown.
   void call(ncclResult_t r, const char* what) {
     if (r == ncclInProgress) {
-      settle(what);
+      settle(what, coll_timeout_);
       return;
     }
     nccl_check(r, what);
@@ -134,10 +150,12 @@ class RcclComm {
                            (hipStream_t)stream),
          "ncclReduceScatter");
   }
+  // "" while healthy: ncclInProgress (a non-blocking call still settling) is not an error
   std::string async_error() {
+    if (!comm_) return "communicator aborted";
     ncclResult_t r = ncclSuccess;
     ncclCommGetAsyncError(comm_, &r);
-    return r == ncclSuccess ? std::string() : std::string(ncclGetErrorString(r));
+    return (r == ncclSuccess || r == ncclInProgress) ? std::string() : std::string(ncclGetErrorString(r));
   }
   void abort() {
     if (comm_) {
@@ -150,8 +168,8 @@ class RcclComm {
   int world() const { return world_; }
 
  private:
-  // Poll the communicator's state until it leaves ncclInProgress; bounded by timeout_.
-  void settle(const char* what) {
+  // Poll the communicator's state until it leaves ncclInProgress; bounded by `timeout`.
+  void settle(const char* what, double timeout) {
     const auto t0 = std::chrono::steady_clock::now();
     for (;;) {
       ncclResult_t st = ncclSuccess;
@@ -160,15 +178,15 @@ class RcclComm {
         nccl_check(st, what);
         return;
       }
-      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_)
-        throw std::runtime_error(std::string(what) + ": timed out after " + std::to_string(timeout_) +
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout)
+        throw std::runtime_error(std::string(what) + ": timed out after " + std::to_string(timeout) +
                                  " s (did every rank join?)");
       std::this_thread::sleep_for(std::chrono::microseconds(200));
     }
   }
   ncclComm_t comm_ = nullptr;
   int rank_, world_, device_;
-  double timeout_;
+  double timeout_, coll_timeout_;
 };
 
 // Bucketed gradient all-reduce over RCCL.  The readiness logic lives in
@@ -201,49 +219,100 @@ class BucketReducer {
   }
   ~BucketReducer() {
     for (auto& e : ev_) hipEventDestroy(e);
+    for (auto& e : tev_) hipEventDestroy(e);
     hipEventDestroy(done_);
     hipStreamDestroy(comm_stream_);
   }
-  void begin() {
+  // Per-bucket timing (diagnostics, off by default and never inside a captured step): timing-enabled events
+  //   t_begin (compute stream at begin()), per bucket: ready = each producer stream's mark event, start / end
+  //   around the all-reduce on the comm stream, and t_bwd (compute stream at finish(), every gradient written).
+  // timings() turns them into milliseconds relative to t_begin; it synchronises on the events.
+  void set_timing(bool on) {
+    if (on && tev_.empty()) {
+      const int nb = (int)off_.size();
+      tev_.resize((size_t)nb * (BucketSchedule::kMaxStreams + 2) + 2);
+      for (auto& e : tev_) hip_check(hipEventCreate(&e), "hipEventCreate(timing)");
+    }
+    timing_ = on;
+  }
+  void begin(uintptr_t stream) {
     sched_.begin();
     launched_.clear();
+    if (timing_) {
+      nready_.assign(off_.size(), 0);
+      hip_check(hipEventRecord(tev_[tbegin()], (hipStream_t)stream), "record t_begin");
+    }
   }
   // Returns the number of buckets launched by this call.
   int mark_ready(const std::vector<int>& params, uintptr_t stream) {
     std::vector<int> touched;
     const std::vector<int> ready = sched_.mark(params, (uint64_t)stream, &touched);
-    for (int b : touched)
-      hip_check(hipEventRecord(ev_[(size_t)b * BucketSchedule::kMaxStreams + sched_.slot_of(b, (uint64_t)stream)],
-                               (hipStream_t)stream),
+    for (int b : touched) {
+      const int slot = sched_.slot_of(b, (uint64_t)stream);
+      hip_check(hipEventRecord(ev_[(size_t)b * BucketSchedule::kMaxStreams + slot], (hipStream_t)stream),
                 "record bucket");
+      if (timing_) {
+        hip_check(hipEventRecord(tev_[tready(b, slot)], (hipStream_t)stream), "record t_ready");
+        nready_[b] = std::max(nready_[b], slot + 1);
+      }
+    }
     for (int b : ready) launch(b);
     return (int)ready.size();
   }
   void finish(uintptr_t compute_stream) {
+    if (timing_) hip_check(hipEventRecord(tev_[tbwd()], (hipStream_t)compute_stream), "record t_bwd");
     for (int b : sched_.finish()) launch(b);
     hip_check(hipEventRecord(done_, comm_stream_), "record done");
     hip_check(hipStreamWaitEvent((hipStream_t)compute_stream, done_, 0), "wait done");
+  }
+  // [(bucket, ready_ms, start_ms, end_ms)] of the last timed step (ms after begin()) and the backward end (ms):
+  // ready = the last producer of the bucket done, start/end = its all-reduce on the comm stream.
+  std::pair<std::vector<std::tuple<int, double, double, double>>, double> timings() {
+    std::vector<std::tuple<int, double, double, double>> out;
+    if (tev_.empty()) return {out, -1.0};
+    auto ms = [&](hipEvent_t e) {
+      hip_check(hipEventSynchronize(e), "event sync");
+      float v = 0.f;
+      hip_check(hipEventElapsedTime(&v, tev_[tbegin()], e), "elapsed");
+      return (double)v;
+    };
+    for (int b : launched_) {
+      double rdy = 0.0;
+      for (int i = 0; i < nready_[b]; ++i) rdy = std::max(rdy, ms(tev_[tready(b, i)]));
+      out.emplace_back(b, rdy, ms(tev_[tstart(b)]), ms(tev_[tend(b)]));
+    }
+    return {out, ms(tev_[tbwd()])};
   }
   uintptr_t comm_stream() const { return (uintptr_t)comm_stream_; }
   int num_buckets() const { return (int)off_.size(); }
   std::vector<int> launched() const { return launched_; }
 
  private:
+  size_t per() const { return BucketSchedule::kMaxStreams + 2; }
+  size_t tready(int b, int slot) const { return (size_t)b * per() + slot; }
+  size_t tstart(int b) const { return (size_t)b * per() + BucketSchedule::kMaxStreams; }
+  size_t tend(int b) const { return (size_t)b * per() + BucketSchedule::kMaxStreams + 1; }
+  size_t tbegin() const { return off_.size() * per(); }
+  size_t tbwd() const { return off_.size() * per() + 1; }
+
   void launch(int b) {
     const auto& ss = sched_.streams(b);
     for (int i = 0; i < (int)ss.size(); ++i)
       hip_check(hipStreamWaitEvent(comm_stream_, ev_[(size_t)b * BucketSchedule::kMaxStreams + i], 0), "wait bucket");
+    if (timing_) hip_check(hipEventRecord(tev_[tstart(b)], comm_stream_), "record t_start");
     comm_.call(ncclAllReduce(arena_ + off_[b], arena_ + off_[b], cnt_[b], ncclFloat32, ncclSum, comm_.raw(),
                              comm_stream_),
                "bucket allreduce");
+    if (timing_) hip_check(hipEventRecord(tev_[tend(b)], comm_stream_), "record t_end");
     launched_.push_back(b);
   }
   RcclComm& comm_;
   float* arena_;
   std::vector<size_t> off_, cnt_;
   BucketSchedule sched_;
-  std::vector<hipEvent_t> ev_;
-  std::vector<int> launched_;
+  std::vector<hipEvent_t> ev_, tev_;
+  std::vector<int> launched_, nready_;
+  bool timing_ = false;
   hipEvent_t done_;
   hipStream_t comm_stream_;
 };
@@ -371,15 +440,18 @@ void register_rccl(py::module_& m) {
   py::class_<RcclComm>(m, "RcclComm")
       // uid arrives as std::string: converted from bytes BEFORE the GIL is
       // released (ncclCommInitRank blocks until every rank has joined)
-      .def(py::init([](int rank, int world, std::string uid, int device, double init_timeout_s) {
-             return new RcclComm(rank, world, uid, device, init_timeout_s);
+      .def(py::init([](int rank, int world, std::string uid, int device, double init_timeout_s,
+                       double coll_timeout_s) {
+             return new RcclComm(rank, world, uid, device, init_timeout_s, coll_timeout_s);
            }),
            py::arg("rank"), py::arg("world"), py::arg("uid"), py::arg("device"), py::arg("init_timeout_s") = 300.0,
+           py::arg("coll_timeout_s") = 120.0,
            py::call_guard<py::gil_scoped_release>())
-      .def("allreduce", &RcclComm::allreduce)
-      .def("broadcast", &RcclComm::broadcast)
-      .def("allgather", &RcclComm::allgather)
-      .def("reduce_scatter", &RcclComm::reduce_scatter)
+      // collectives may settle a non-blocking call (bounded): the GIL is released meanwhile
+      .def("allreduce", &RcclComm::allreduce, py::call_guard<py::gil_scoped_release>())
+      .def("broadcast", &RcclComm::broadcast, py::call_guard<py::gil_scoped_release>())
+      .def("allgather", &RcclComm::allgather, py::call_guard<py::gil_scoped_release>())
+      .def("reduce_scatter", &RcclComm::reduce_scatter, py::call_guard<py::gil_scoped_release>())
       .def("async_error", &RcclComm::async_error)
       .def("abort", &RcclComm::abort)
       .def_property_readonly("rank", &RcclComm::rank)
@@ -387,9 +459,11 @@ void register_rccl(py::module_& m) {
   py::class_<BucketReducer>(m, "BucketReducer")
       .def(py::init<RcclComm&, uintptr_t, std::vector<size_t>, std::vector<size_t>, std::vector<int>, int>(),
            py::keep_alive<1, 2>())
-      .def("begin", &BucketReducer::begin)
-      .def("mark_ready", &BucketReducer::mark_ready)
-      .def("finish", &BucketReducer::finish)
+      .def("begin", &BucketReducer::begin, py::arg("stream") = 0)
+      .def("mark_ready", &BucketReducer::mark_ready, py::call_guard<py::gil_scoped_release>())
+      .def("finish", &BucketReducer::finish, py::call_guard<py::gil_scoped_release>())
+      .def("set_timing", &BucketReducer::set_timing)
+      .def("timings", &BucketReducer::timings, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("launched", &BucketReducer::launched)
       .def_property_readonly("comm_stream", &BucketReducer::comm_stream)
       .def_property_readonly("num_buckets", &BucketReducer::num_buckets);

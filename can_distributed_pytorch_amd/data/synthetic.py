@@ -157,4 +157,4 @@ def expected_flops_per_image(h: int, w: int) -> float:
 
 
 __all__ = ["make_synthetic_batch", "make_synthetic_batch_gpu", "SyntheticGPULoader", "synthetic_points", "density_from_points_fixed",
-           "expected_flops_per_image", "IMAGENET_MEAN", "IMAGENET_STD", "math"]
+           "expected_flops_per_image", "IMAGENET_MEAN", "IMAGENET_STD"]

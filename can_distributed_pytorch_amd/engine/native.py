@@ -84,6 +84,7 @@ class NativeStepper:
         self.bucket_mb = bucket_mb
         self.comm_timing = False
         self._comm_events = []
+        self._bucket_reports = []
         self.reducer = reducer
         if self.reducer is None and (world > 1 or reducer_transport is not None):
             from ..parallel.reducer import BucketedReducer
@@ -129,14 +130,15 @@ class NativeStepper:
             loss, et, d_b6 = ex.head_train(b6, gt, self.grads, lscale=sc[0:1] if sc is not None else None,
                                            flags=self.flags)
         red = self.reducer
+        timing = self.comm_timing and self.device.type == "cuda"
         if red is not None:
+            red.set_timing(timing)
             red.begin()
             red.mark_ready([ex.head_w_index, ex.head_b_index])
         with trace_range("cannet/backward"):
             ex.backward_features(sv, d_b6, self.grads, on_grad_ready=(red.mark_ready if red is not None else None),
                                  dscale=sc[1:2] if sc is not None else None)
         del sv
-        timing = self.comm_timing and self.device.type == "cuda"
         if timing:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -148,6 +150,8 @@ class NativeStepper:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record()
             self._comm_events.append((e0, e1))
+            if red is not None:
+                self._bucket_reports.append(red.timings())
         if sc is not None:
             # after the all-reduce every rank holds the same gradients -> the same verdict
             self.flags[2:3].zero_()
@@ -176,6 +180,15 @@ class NativeStepper:
         if reset:
             self._comm_events = []
         return v
+
+    def comm_report(self, reset: bool = True) -> Optional[dict]:
+        """Per-bucket all-reduce timing of the last step run with ``comm_timing`` (BucketedReducer.timings: when
+        each bucket's gradients were ready, when its all-reduce started / ended, relative to the start of the
+        backward, and how long the all-reduce ran past the backward)."""
+        t = [x for x in self._bucket_reports if x is not None]
+        if reset:
+            self._bucket_reports = []
+        return t[-1] if t else None
 
     # ------------------------------------------------------------ public
     def step(self, img, gt):

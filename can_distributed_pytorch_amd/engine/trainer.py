@@ -85,9 +85,80 @@ class Fp32Stepper(TorchStepper):
         super().__init__(device, dtype="fp32", channels_last=False, **kw)
 
 
+class ArenaStepper:
+    """This framework's data-parallel engine on the plain-ATen CANNet: the CPU / gloo rehearsal of the native step's
+    distributed path (engine/native.py), used by ``bench.py --device cpu`` and the multi-process CPU tests.
+
+    Same structure as the native step: fp32 parameters and gradients in one flat arena laid out in gradient-ready
+    order (utils/flat.py), the bucketed reducer (parallel/reducer.py) driven by post-accumulate-grad hooks so
+    buckets are all-reduced while autograd still runs, the loss and its non-finite flag in one 2-element collective,
+    1/world folded into the SGD update (momentum 0.95, train.py:63,126 of the reference), the update skipped on a
+    non-finite loss on every rank alike, and the init-time parameter sync as one broadcast of the arena."""
+    exec_backend = "torch"
+
+    def __init__(self, device="cpu", world=1, lr=1e-7, momentum=0.95, model=None, bucket_mb: float = 25.0):
+        from ..models.cannet import grad_ready_order
+        from ..parallel.reducer import BucketedReducer
+        from ..utils.flat import FlatArena
+        self.device = torch.device(device)
+        self.model = (model or CANNet(backend=self.exec_backend)).to(self.device)
+        self.model.exec_backend = self.exec_backend
+        self.world = world
+        self.lr = lr * world                       # train.py:25 linear scaling
+        self.momentum = momentum
+        self.params = list(self.model.parameters())
+        order = grad_ready_order(self.model)
+        self.arena = FlatArena(self.params, self.device, order=order)
+        self.mom = torch.zeros_like(self.arena.data)
+        self.reducer = BucketedReducer(self.arena, order, bucket_mb=bucket_mb, transport="torch")
+        self.reducer.attach_hooks()
+        self.flags = torch.zeros(2, dtype=torch.float32, device=self.device)
+        self.crit = torch.nn.MSELoss(reduction="sum")
+        self.comm_timing = False
+        self._timings = []
+        self._loss = None
+        if world > 1:
+            self.reducer.broadcast_arena(0)
+
+    def step(self, img, gt):
+        red = self.reducer
+        red.set_timing(self.comm_timing)
+        self.arena.grad.zero_()
+        self.arena.attach_grads()                  # autograd accumulates into the arena views in place
+        red.begin()
+        et = self.model(img.to(self.device))
+        loss = self.crit(et, gt.to(self.device))
+        loss.backward()
+        red.finish()
+        if self.comm_timing:
+            self._timings.append(red.timings())
+        with torch.no_grad():
+            self.flags[0] = 0.0 if bool(torch.isfinite(loss)) else 1.0
+            self.flags[1] = loss.detach()
+            red.allreduce_scalars(self.flags)
+            if self.flags[0] == 0:
+                # buf = m * buf + g / W ; p -= lr * buf   (torch.optim.SGD semantics, zero-initialised buffer)
+                self.mom.mul_(self.momentum).add_(self.arena.grad, alpha=1.0 / self.world)
+                self.arena.data.add_(self.mom, alpha=-self.lr)
+        self._loss = self.flags[1:2] / self.world
+        return self._loss
+
+    def comm_report(self, reset: bool = True) -> Optional[dict]:
+        """The last timed step's per-bucket all-reduce report (BucketedReducer.timings)."""
+        t = [x for x in self._timings if x is not None]
+        if reset:
+            self._timings = []
+        return t[-1] if t else None
+
+    def last_loss(self) -> Optional[float]:
+        return None if self._loss is None else float(self._loss.reshape(-1)[0])
+
+
 def build_trainer(impl="hip", dtype="bf16", device="cuda", world=1, lr=1e-7, batch=8,
                   height=768, width=1024, graph=True, model=None, bucket_mb: float = 25.0,
                   reducer_transport: Optional[str] = None):
+    if impl == "arena":
+        return ArenaStepper(device, world=world, lr=lr, model=model, bucket_mb=bucket_mb)
     if impl == "torch":
         return TorchStepper(device, dtype=dtype, world=world, lr=lr, model=model, bucket_mb=bucket_mb)
     if dtype == "fp32":

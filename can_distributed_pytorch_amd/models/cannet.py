@@ -195,6 +195,23 @@ def cannet_forward_reference(model: CANNet, x: torch.Tensor) -> torch.Tensor:
     return model.output_layer(y)
 
 
+def grad_ready_order(model: CANNet) -> List[int]:
+    """model.parameters() indices in the order a backward produces their gradients: output head, backend (last
+    layer first), conv{S}_2, conv{S}_1, frontend (last layer first).  The native executor's schedule
+    (ops/executor.py CANNetExecutor.grad_ready_order) and the flat gradient arena follow it, so DDP-style buckets
+     are contiguous slices."""
+    pid = {id(p): i for i, p in enumerate(model.parameters())}
+    order = [pid[id(model.output_layer.weight)], pid[id(model.output_layer.bias)]]
+    for m in reversed(model.backend_convs()):
+        order += [pid[id(m.weight)], pid[id(m.bias)]]
+    order += [pid[id(getattr(model, f"conv{s}_2").weight)] for s in CONTEXT_SCALES]
+    order += [pid[id(getattr(model, f"conv{s}_1").weight)] for s in CONTEXT_SCALES]
+    for m in reversed(model.frontend_convs()):
+        order += [pid[id(m.weight)], pid[id(m.bias)]]
+    rest = [i for i in range(len(pid)) if i not in set(order)]       # BN variant: its affine params last
+    return order + rest
+
+
 def strip_module_prefix(state_dict) -> "collections.OrderedDict[str, torch.Tensor]":
     out = collections.OrderedDict()
     for k, v in state_dict.items():

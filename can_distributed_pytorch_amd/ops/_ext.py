@@ -36,13 +36,36 @@ def available() -> bool:
     return load() is not None
 
 
+_checked = False
+
+
+def check_source_hash(m) -> None:
+    """Refuse a binary that was not built from the csrc/ sources in this tree (a stale or foreign _C)."""
+    from .. import build_native
+    files = build_native.source_files()
+    if not files:                      # installed without sources: nothing to compare against
+        return
+    want = build_native.source_hash(files)
+    got = m.src_hash()
+    if got != want:
+        raise RuntimeError(
+            f"stale native extension: {m.__file__} was built from csrc/ sources with sha256 {got[:16]}..., the tree's "
+            f"sources hash to {want[:16]}...; rebuild with `python -m can_distributed_pytorch_amd.build_native`")
+
+
 def require():
+    global _checked
     m = load()
     if m is None:
         raise RuntimeError(
             "can_distributed_pytorch_amd native extension (_C) is not built: run "
             "`python -m can_distributed_pytorch_amd.build_native` (hipcc --offload-arch=gfx950). "
             f"Import error: {_err}")
+    if not _checked:
+        check_source_hash(m)
+        from . import dispatch
+        dispatch.apply(dispatch.current())    # the validated $CANNET_DISPATCH config, pushed once
+        _checked = True
     return m
 
 

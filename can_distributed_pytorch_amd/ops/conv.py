@@ -16,12 +16,12 @@ Weight layouts (packed from the fp32 master weights [Co][Ci][kh][kw]):
 """
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
 
 from . import _ext
+from . import dispatch
 
 EPI_BIAS_RELU, EPI_MASK, EPI_NONE, EPI_BIAS, EPI_SIGMOID, EPI_POOLBWD = 0, 1, 2, 3, 4, 5
 BF16 = torch.bfloat16
@@ -191,17 +191,9 @@ def conv_dgrad_with_bias(dy: torch.Tensor, wpack: torch.Tensor, *, ksize: int, d
     n, h, w, _ = dy.shape
     co = wpack.shape[0]
     bp = torch.empty(bias_part_capacity(n, h, w), co, dtype=torch.float32, device=dy.device)
-    out, part = conv_igemm(dy, wpack, None, ksize=ksize, dil=dil, epi=epi, mask=mask, tile=tile, bias_part=bp)
-    if part is not None and part.shape[0] > BIAS_ROWS and os.environ.get("CANNET_BIAS_PRE_MAIN", "0") == "1":
-        # CANNET_BIAS_PRE_MAIN=1: long partial lists folded right here, on the producer's (critical-path) stream.
-        # Default: conv_wgrad folds them on the weight-gradient stream after its GEMM; here the short launch waited
-        # 85-345 us for CUs behind the weight-gradient GEMM (profiles/r3/ab_bias_prereduce.txt)
-        C = _ext.require()
-        red = torch.empty(BIAS_ROWS, co, dtype=torch.float32, device=dy.device)
-        g = C.bias_rows_reduce(part.data_ptr(), red.data_ptr(), part.shape[0], co, BIAS_ROWS,
-                               _ext.stream_ptr(dy.device))
-        part = red[:g]
-    return out, part
+    # long partial lists are folded by conv_wgrad on the weight-gradient stream after its GEMM (folded here, on the
+    # producer's critical-path stream, the short launch waited 85-345 us for CUs, profiles/r3/ab_bias_prereduce.txt)
+    return conv_igemm(dy, wpack, None, ksize=ksize, dil=dil, epi=epi, mask=mask, tile=tile, bias_part=bp)
 
 
 def _check_codes(codes: Optional[torch.Tensor], pooled_shape) -> None:
@@ -315,8 +307,8 @@ def _ctx_wgrad_cus() -> int:
     critical-path context backward (bilinear-transpose row / cell passes, ctx_bwd_final) runs on the compute stream;
     a grid of one 512-thread, 256-VGPR block per CU leaves those memory-bound kernels no CU until it drains.
     224 of 256 measured best (profiles/r2/ab_ctx_wgrad_cus.txt: 441.7-442.4 img/s vs 438.9-440.9 for 256,
-    worse at 192 / 160); CANNET_CTX_WGRAD_CUS overrides."""
-    return int(os.environ.get("CANNET_CTX_WGRAD_CUS", "224"))
+    worse at 192 / 160); dispatch ctx_wgrad_cus selects."""
+    return dispatch.current().ctx_wgrad_cus
 
 
 def wgrad_1x1_batched_plan(m: int, nb: int, ci: int, co: int, ncu: int = 0):
@@ -367,27 +359,6 @@ def conv_wgrad_1x1_batched(dy: torch.Tensor, x: torch.Tensor, dws, *, ws: "Wgrad
                              _ext.stream_ptr(x.device))
 
 
-# ----------------------------------------------------------------------------------------------
-# conv1_2 with conv1_1 recomputed.  X2 = relu(conv1_1(img) + b1) (64 channels at full resolution,
-# 805 MB per 8 x 768 x 1024 batch) is never stored: the conv1_2 forward rebuilds its X2 halo from
-# the NHWC4 image, the data gradient rebuilds conv1_1's ReLU mask, and the weight gradient rebuilds
-# its X2 tiles per stage.  ~4.5 GB less HBM traffic per training step at batch 8.
-# ----------------------------------------------------------------------------------------------
-F1_WGRAD_SLICES = 512
-
-
-def _check_f1(img: torch.Tensor, w1pack: torch.Tensor, b1: torch.Tensor, dt):
-    if img.dim() != 4 or img.shape[-1] != 4:
-        raise ValueError("img must be the NHWC4 network input [N,H,W,4]")
-    _check_act(img, "img", dtype=dt)
-    if tuple(w1pack.shape) != (64, 64) or w1pack.dtype != dt or not w1pack.is_contiguous():
-        raise ValueError("w1pack must be the packed first-layer weight [64,64] of the activation dtype")
-    if b1.dtype != torch.float32 or b1.numel() != 64 or not b1.is_contiguous():
-        raise ValueError("b1 must be contiguous fp32 [64]")
-    if img.shape[2] % 2:
-        raise ValueError("W must be even")
-
-
 def conv_pool_fwd_ok(x: torch.Tensor, cout: int, ksize: int, tile: int = 0) -> bool:
     """Whether conv_pool_fwd covers this layer: H even and W a multiple of half the kernel's pixel tile."""
     n, h, w, ci = x.shape
@@ -435,60 +406,6 @@ def conv_pool_fwd(x: torch.Tensor, wpack: torch.Tensor, bias: torch.Tensor, *, k
                     pooled.data_ptr(), cd.data_ptr() if cd is not None else 0, n, h, w, ci, co, ksize, dil, tile,
                     dt_code(dt), _ext.stream_ptr(x.device))
     return out, pooled, cd
-
-
-def conv_f1(x: Optional[torch.Tensor], wpack: torch.Tensor, bias: Optional[torch.Tensor], img: torch.Tensor,
-            w1pack: torch.Tensor, b1: torch.Tensor, *, epi: int) -> torch.Tensor:
-    """epi=EPI_BIAS_RELU: conv1_2 forward, relu(conv(X2, wpack) + bias) with X2 recomputed from img (x unused).
-    epi=EPI_MASK: conv1_2 data gradient, conv(x = dY, flipped wpack) * (X2 > 0) with X2 recomputed."""
-    C = _ext.require()
-    dt = img.dtype
-    _check_f1(img, w1pack, b1, dt)
-    n, h, w, _ = img.shape
-    if tuple(wpack.shape) != (64, 576) or wpack.dtype != dt or not wpack.is_contiguous():
-        raise ValueError("wpack must be a packed [64, 9*64] conv1_2 weight")
-    if epi == EPI_BIAS_RELU:
-        if bias is None or bias.dtype != torch.float32 or bias.numel() != 64:
-            raise ValueError("bias must be fp32 [64]")
-        xp = 0
-    elif epi == EPI_MASK:
-        if x is None or tuple(x.shape) != (n, h, w, 64):
-            raise ValueError("x (dY) must be [N,H,W,64]")
-        _check_act(x, "x", dtype=dt)
-        xp = x.data_ptr()
-    else:
-        raise ValueError("conv_f1 supports EPI_BIAS_RELU and EPI_MASK")
-    out = torch.empty(n, h, w, 64, dtype=dt, device=img.device)
-    C.conv_f1(xp, wpack.data_ptr(), bias.data_ptr() if bias is not None else 0, img.data_ptr(), w1pack.data_ptr(),
-              b1.data_ptr(), out.data_ptr(), n, h, w, epi, dt_code(dt), _ext.stream_ptr(img.device))
-    return out
-
-
-def conv_wgrad_f1_need(m: int) -> int:
-    return F1_WGRAD_SLICES * 576 * 64 + max(F1_WGRAD_SLICES, 512) * 64
-
-
-def conv_wgrad_f1(dy: torch.Tensor, img: torch.Tensor, w1pack: torch.Tensor, b1: torch.Tensor, dw: torch.Tensor,
-                  db: Optional[torch.Tensor], *, ws: WgradWorkspace, beta: float = 0.0, scale: float = 1.0,
-                  dscale: Optional[torch.Tensor] = None) -> None:
-    """conv1_2 weight / bias gradient with its input X2 = relu(conv1_1(img) + b1) recomputed."""
-    C = _ext.require()
-    dt = dy.dtype
-    _check_act(dy, "dy", 64)
-    _check_f1(img, w1pack, b1, dt)
-    n, h, w, _ = img.shape
-    if tuple(dy.shape) != (n, h, w, 64):
-        raise ValueError("dy must be [N,H,W,64]")
-    if tuple(dw.shape) != (64, 64, 3, 3) or dw.dtype != torch.float32 or not dw.is_contiguous():
-        raise ValueError("dw must be contiguous fp32 [64,64,3,3]")
-    if db is not None and (db.dtype != torch.float32 or db.numel() != 64):
-        raise ValueError("db must be fp32 [64]")
-    s = F1_WGRAD_SLICES
-    buf = ws.reserve(conv_wgrad_f1_need(n * h * w))
-    C.conv_wgrad_f1(dy.data_ptr(), img.data_ptr(), w1pack.data_ptr(), b1.data_ptr(), buf.data_ptr(),
-                    buf.data_ptr() + 4 * s * 576 * 64, dw.data_ptr(), db.data_ptr() if db is not None else 0, n, h, w,
-                    s, float(beta), float(scale), dscale.data_ptr() if dscale is not None else 0, dt_code(dt),
-                    _ext.stream_ptr(img.device))
 
 
 def w1g_slab_cap(device) -> int:

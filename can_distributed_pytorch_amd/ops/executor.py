@@ -32,7 +32,6 @@ Two ways in:
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional, Sequence
 
@@ -41,6 +40,7 @@ import torch.nn as nn
 
 from . import _ext
 from . import conv as C
+from . import dispatch
 from ..models.cannet import CONTEXT_SCALES
 
 BF16 = torch.bfloat16
@@ -93,7 +93,6 @@ class CANNetExecutor:
         self._pack_desc = None          # device descriptor rows of the batched pack launch
         self._pack_desc_ptrs = None
         self.ws = None
-        self.ws_main = None             # conv1_1 weight-gradient slabs when it runs on the compute stream
         self._w1g_buf = None            # conv1_1 weight-gradient slabs of the fused conv1_2 data gradient
         self.stream_override = None
         self._side = None
@@ -194,14 +193,9 @@ class CANNetExecutor:
         need = max(need, self.ws.plan(n * hh * ww, 512, 512, 1, False)[3])
         need = max(need, self.ws.plan(n * hh * ww, 512, 4 * 512, 1, False)[3])    # linearised context dW2cat
         need = max(need, max(C.wgrad_1x1_batched_plan(n * hh * ww, 4, 512, 512, ncu=c)[2] for c in (128, 192, 224, 256)))
-        need = max(need, C.conv_wgrad_f1_need(n * h * w))
         self.ws.reserve(need)
-        if os.environ.get("CANNET_W1G", "1") != "0":
+        if dispatch.current().w1g:
             self._w1g_slabs(self.head.weight.device)
-        if self._f0_wgrad_main():
-            if self.ws_main is None:
-                self.ws_main = C.WgradWorkspace(self.head.weight.device)
-            self.ws_main.reserve(self.ws_main.plan(n * h * w, 4, self.front[0].cout, 3, True)[3])
         return self.ws
 
     def _w1g_ok(self, x) -> bool:
@@ -209,7 +203,7 @@ class CANNetExecutor:
         weight-gradient launch on the side stream).  Measured 453.5 -> 456.7 img/s, peak HBM 8.75 -> 7.95 GB
         (profiles/r2/ab_w1g.txt)."""
         f0, f1 = self.front[0], self.front[1]
-        return (os.environ.get("CANNET_W1G", "1") != "0" and f0.first and f0.cout == 64 and f1.cin == 64
+        return (dispatch.current().w1g and f0.first and f0.cout == 64 and f1.cin == 64
                 and f1.cout == 64 and not f0.pool_after and x.dim() == 4 and x.shape[-1] == 64)
 
     def _w1g_slabs(self, device):
@@ -219,11 +213,6 @@ class CANNetExecutor:
                              torch.empty(cap, 64, dtype=torch.float32, device=device))
         return self._w1g_buf
 
-    @staticmethod
-    def _f0_wgrad_main() -> bool:
-        """CANNET_F0_WGRAD_MAIN=1: conv1_1's weight gradient on the compute stream (see backward_features)."""
-        return os.environ.get("CANNET_F0_WGRAD_MAIN", "0") == "1"
-
     # ----------------------------------------------------------- forward
     def _conv(self, s: ConvSpec, x, epi=C.EPI_BIAS_RELU):
         fwd, _ = self.packs[id(s.module.weight)]
@@ -231,9 +220,9 @@ class CANNetExecutor:
 
     def _pool_fused(self, s: ConvSpec, x) -> bool:
         """The 2x2 max-pool after this conv runs in the conv's epilogue (LDS-DMA kernels; conv1_2: the halo
-        kernel's epilogue through an LDS staging tile).  CANNET_POOL_FWD_FUSED=0: separate pool kernel."""
+        kernel's epilogue through an LDS staging tile).  Dispatch pool_fwd_fused = 0: separate pool kernel."""
         return (s.pool_after and not s.first and s.dil == 1 and (s.cin != 64 or s.cout == 64)
-                and os.environ.get("CANNET_POOL_FWD_FUSED", "1") != "0" and C.conv_pool_fwd_ok(x, s.cout, s.ksize))
+                and dispatch.current().pool_fwd_fused and C.conv_pool_fwd_ok(x, s.cout, s.ksize))
 
     def _maxpool(self, x):
         """(pooled, max-pool codes): the codes replace the pool input in the saved state."""
@@ -261,36 +250,16 @@ class CANNetExecutor:
         self.C.img_to_nhwc4(img.data_ptr(), x4.data_ptr(), n, h, w, self.dt, self._stream())
         return x4
 
-    def _f1_fused(self) -> bool:
-        """Opt-in (CANNET_F1_FUSED=1): conv1_1's output is recomputed inside conv1_2's kernels instead
-        of being stored.  Measured at 768x1024 batch 8 (profiles/r1_native/f1_recompute.txt): forward
-        -0.27 ms and data gradient even, but the weight gradient's per-stage recompute of the 4 x 66
-        halo (2x the 2 x 64 output rows it feeds) costs +0.38 ms, so the stored path stays the default."""
-        f0, f1 = self.front[0], self.front[1]
-        return (os.environ.get("CANNET_F1_FUSED", "0") == "1" and f0.first and f0.cout == 64 and f1.cin == 64 and
-                f1.cout == 64 and f1.ksize == 3 and f1.dil == 1)
-
-    def _f1_args(self):
-        f0 = self.front[0]
-        return self.packs[id(f0.module.weight)][0], f0.module.bias.detach()
-
     def forward_features(self, img, save: bool):
         """Runs everything up to the last backend ReLU. Returns (b6 [N,h,w,64], saved dict)."""
         self.refresh_packs()
         sv = {} if save else None
         x = self._img(img)
-        acts = []   # conv inputs of the frontend (conv1_2's is the image too when conv1_1 is recomputed)
+        acts = []   # conv inputs of the frontend
         pre_pool = {}
-        f1 = self._f1_fused()
         for s in self.front:
             acts.append(x)
-            if f1 and s.idx == 0:
-                continue                     # conv1_1 runs inside conv1_2's kernels
-            if f1 and s.idx == 1:
-                w1, b1 = self._f1_args()
-                fwd, _ = self.packs[id(s.module.weight)]
-                y = C.conv_f1(None, fwd, s.module.bias.detach(), acts[0], w1, b1, epi=C.EPI_BIAS_RELU)
-            elif self._pool_fused(s, x):
+            if self._pool_fused(s, x):
                 # conv + ReLU + pool in one kernel; only the pooled map and the max-pool codes are written
                 # (the full-resolution output is never stored: the backward needs the codes alone)
                 fwd, _ = self.packs[id(s.module.weight)]
@@ -314,14 +283,14 @@ class CANNetExecutor:
             back_in.append(x)
             x = self._conv(s, x)
         if save:
-            sv.update(front_in=acts, pre_pool=pre_pool, fv=fv, ctx=ctx_saved, back_in=back_in, b6=x, f1=f1)
+            sv.update(front_in=acts, pre_pool=pre_pool, fv=fv, ctx=ctx_saved, back_in=back_in, b6=x)
         return x, sv
 
     @staticmethod
     def _ctx_linear(fv) -> bool:
-        """The context module as one GEMM each way (conv_igemm.hip "Linearised context module"); CANNET_CTX_LINEAR=0
-        or a map narrower than 64 columns: the direct per-scale form (expand -> 4 sigmoid GEMMs -> fuse)."""
-        return os.environ.get("CANNET_CTX_LINEAR", "1") != "0" and C.ctx_linear_ok(fv)
+        """The context module as one GEMM each way (conv_igemm.hip "Linearised context module"); dispatch ctx_linear =
+        0 or a map narrower than 64 columns: the direct per-scale form (expand -> 4 sigmoid GEMMs -> fuse)."""
+        return bool(dispatch.current().ctx_linear) and C.ctx_linear_ok(fv)
 
     def _context_fwd(self, fv, save):
         if self._ctx_linear(fv):
@@ -371,8 +340,8 @@ class CANNetExecutor:
 
     @staticmethod
     def _ctx_batched(h, w):
-        """The four conv{S}_2 1x1 convs as one batched launch (CANNET_CTX_BATCHED=0: four launches)."""
-        return h >= 2 and w >= 2 and os.environ.get("CANNET_CTX_BATCHED", "1") != "0"
+        """The four conv{S}_2 1x1 convs as one batched launch (dispatch ctx_batched = 0: four launches)."""
+        return h >= 2 and w >= 2 and bool(dispatch.current().ctx_batched)
 
     def _ctx1_ptrs(self):
         ws = [self.ctx1[sc].weight for sc in CONTEXT_SCALES]
@@ -414,8 +383,8 @@ class CANNetExecutor:
         # launch need not re-read dY for db (the bias column sums were ~1 ms/step of weight-gradient-stream
         # time).  Round 2 measured it negative (421-423 vs 427 img/s, profiles/r2/README.md); after the round-3
         # kernel changes it is ahead in every interleaved round (485.5-485.8 vs 483.3-485.1 img/s,
-        # profiles/r3/ab_bias_fused.txt), so it is the default; CANNET_BIAS_FUSED=0 re-reads dY
-        fuse_bias = os.environ.get("CANNET_BIAS_FUSED", "1") == "1"
+        # profiles/r3/ab_bias_fused.txt), so it is the default; dispatch bias_fused = 0 re-reads dY
+        fuse_bias = bool(dispatch.current().bias_fused)
 
         def wg(spec_or_w, dy, x, ksize, dil, first, wi, bi, bp=None):
             # bp: bias partials of dy summed by the data-gradient epilogue that wrote it (None: the weight-
@@ -448,32 +417,6 @@ class CANNetExecutor:
         bp = None
         for s in reversed(self.front):
             x = sv["front_in"][s.idx]
-            if sv.get("f1") and s.idx == 1:
-                # conv1_2 with conv1_1's output recomputed from the image (x) in both kernels
-                w1, b1 = self._f1_args()
-                _, dgr = self.packs[id(s.module.weight)]
-                dy2 = dy
-
-                def run_f1(dy2=dy2, x=x, s=s):
-                    C.conv_wgrad_f1(dy2, x, w1, b1, grads[s.w_index], grads[s.b_index], ws=ws, beta=beta,
-                                    scale=scale, dscale=dscale)
-                    ready([s.w_index, s.b_index])
-                self._on_side(side, run_f1, hold, dy2, x)
-                dy, bp = C.conv_f1(dy, dgr, None, x, w1, b1, epi=C.EPI_MASK), None
-                continue
-            if s.idx == 0 and side is not None and self._f0_wgrad_main():
-                # conv1_1's weight gradient on the compute stream, which is otherwise idle once conv1_2's data
-                # gradient is done: it overlaps the tail of conv1_2's (longer) weight gradient on the side stream
-                # instead of queueing behind it.  Own slab workspace: the side stream's is still in use.
-                if self.ws_main is None:
-                    self.ws_main = C.WgradWorkspace(dy.device)
-                C.conv_wgrad(dy, x, grads[s.w_index], grads[s.b_index], ksize=3, dil=1, first=s.first,
-                             ws=self.ws_main, beta=beta, scale=scale, dscale=dscale, bias_partials=bp)
-                # join before marking ready: the bucket holding conv1_1 also holds side-stream gradients, and a
-                # transport that orders its all-reduce after the marking stream must see them too
-                torch.cuda.current_stream(d_b6.device).wait_stream(side)
-                ready([s.w_index, s.b_index])
-                break
             wg(s, dy, x, 3, 1, s.first, s.w_index, s.b_index, bp)
             if s.idx == 0:
                 break
@@ -487,7 +430,8 @@ class CANNetExecutor:
                 C.conv_dgrad_w1g(dy, dgr, x, img, grads[prev.w_index], grads[prev.b_index], slabs=sl, bslabs=bsl,
                                  beta=beta, scale=scale, dscale=dscale)
                 if side is not None:
-                    # the bucket holding conv1_1 also holds side-stream gradients (see the F0 path above)
+                    # join before marking ready: the bucket holding conv1_1 also holds side-stream gradients, and a
+                    # transport that orders its all-reduce after the marking stream must see them too
                     torch.cuda.current_stream(d_b6.device).wait_stream(side)
                 ready([prev.w_index, prev.b_index])
                 break
@@ -496,7 +440,7 @@ class CANNetExecutor:
                 # (+ ReLU mask of the pool input) in the conv epilogue: the pooled gradient never
                 # round-trips through memory
                 codes = sv["pre_pool"][prev.idx]
-                if os.environ.get("CANNET_POOLBWD_FUSED", "1") != "0":
+                if dispatch.current().poolbwd_fused:
                     dy, bp = dgrad(dy, dgr, 1, C.EPI_POOLBWD, codes)
                 else:
                     dp = C.conv_igemm(dy, dgr, None, ksize=3, dil=1, epi=C.EPI_NONE)
@@ -511,13 +455,13 @@ class CANNetExecutor:
         """Weight gradients run on a second stream, concurrently with the data-gradient chain (they only
         need the layer's dY and input).  The memory-bound slab reductions / bias column sums and the
         partial last waves of one chain fill the CUs the other leaves idle.  Fork/join through stream
-        waits, so the pattern is hipGraph-capturable; CANNET_WGRAD_STREAM=0 runs everything in order."""
-        if os.environ.get("CANNET_WGRAD_STREAM", "1") == "0" or self.stream_override is not None:
+        waits, so the pattern is hipGraph-capturable; dispatch wgrad_stream = 0 runs everything in order.  (A
+        high-priority side stream measured negative, profiles/r2/ab_side_priority_negative.txt.)"""
+        if not dispatch.current().wgrad_stream or self.stream_override is not None:
             return None
         dev = self.head.weight.device
         if self._side is None or self._side.device != dev:
-            # CANNET_SIDE_PRIORITY=-1: high-priority weight-gradient stream (its work ends the step)
-            self._side = torch.cuda.Stream(dev, priority=int(os.environ.get("CANNET_SIDE_PRIORITY", "0")))
+            self._side = torch.cuda.Stream(dev)
         return self._side
 
     @staticmethod

@@ -19,6 +19,7 @@ with backward, averaged by world size).  Re-designed for MI355X:
 """
 from __future__ import annotations
 
+import time
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -113,6 +114,8 @@ class BucketedReducer:
         self._pending = None
         self._next = 0
         self._works = []
+        self._timing = False
+        self._host_t = None          # torch transport timing: host clock per launched bucket
 
     def _make_comm_agreed(self, dev, group):
         """This rank's RCCL communicator, or None on EVERY rank if any rank failed to create one.  Every step
@@ -147,11 +150,44 @@ class BucketedReducer:
     # --------------------------------------------------------------- step API
     def begin(self):
         if self._native is not None:
-            self._native.begin()
+            from ..ops import _ext
+            self._native.begin(_ext.stream_ptr(self.arena.grad.device))
             return
         self._pending = [len(b.params) for b in self.buckets]
         self._next = 0
         self._works = []
+        if self._timing:
+            self._host_t = {"t0": time.perf_counter(), "launch": {}, "end": {}, "bwd": None}
+
+    # ------------------------------------------------------------- diagnostics
+    def set_timing(self, on: bool):
+        """Per-bucket all-reduce timing for the next steps (diagnostics; not inside a captured step).
+        rccl: hipEvents on the producer / comm streams; torch: host clock around the async works."""
+        self._timing = bool(on)
+        if self._native is not None:
+            self._native.set_timing(self._timing)
+
+    def timings(self) -> Optional[dict]:
+        """The last timed step: per bucket {bucket, mib, ready_ms, start_ms, end_ms} (ms after begin(); ready =
+        its last gradient written, start / end = its all-reduce) and ``backward_end_ms`` (every gradient written);
+        ``exposed_ms`` = how long the last all-reduce ran past the backward (the part not hidden by compute)."""
+        if self._native is not None:
+            rows, bwd = self._native.timings()
+            if bwd < 0:
+                return None
+            bk = [dict(bucket=b, mib=round(self.buckets[b].numel * 4 / MIB, 3), ready_ms=round(r, 4),
+                       start_ms=round(s0, 4), end_ms=round(e, 4)) for b, r, s0, e in rows]
+        else:
+            ht = self._host_t
+            if not ht or ht["bwd"] is None:
+                return None
+            t0 = ht["t0"]
+            bk = [dict(bucket=b, mib=round(self.buckets[b].numel * 4 / MIB, 3),
+                       ready_ms=round(1e3 * (ht["launch"][b] - t0), 4), start_ms=round(1e3 * (ht["launch"][b] - t0), 4),
+                       end_ms=round(1e3 * (ht["end"].get(b, ht["launch"][b]) - t0), 4)) for b in sorted(ht["launch"])]
+            bwd = 1e3 * (ht["bwd"] - t0)
+        last_end = max((r["end_ms"] for r in bk), default=bwd)
+        return {"buckets": bk, "backward_end_ms": round(bwd, 4), "exposed_ms": round(max(0.0, last_end - bwd), 4)}
 
     def mark_ready(self, params: Sequence[int]):
         if self._native is not None:
@@ -170,22 +206,28 @@ class BucketedReducer:
             self._next += 1
 
     def _launch(self, b: int):
+        if self._timing and self._host_t is not None:
+            self._host_t["launch"][b] = time.perf_counter()
         if self.world < 2:                        # a 1-rank all-reduce is the identity
             return
         bk = self.buckets[b]
         view = self.arena.grad[bk.start:bk.end]
-        self._works.append(dist.all_reduce(view, group=self.group, async_op=True))
+        self._works.append((b, dist.all_reduce(view, group=self.group, async_op=True)))
 
     def finish(self):
         if self._native is not None:
             from ..ops import _ext
             self._native.finish(_ext.stream_ptr(self.arena.grad.device))
             return
+        if self._timing and self._host_t is not None:
+            self._host_t["bwd"] = time.perf_counter()
         while self._next < len(self.buckets):
             self._launch(self._next)
             self._next += 1
-        for w in self._works:
+        for b, w in self._works:
             w.wait()
+            if self._timing and self._host_t is not None:
+                self._host_t["end"][b] = time.perf_counter()
         self._works = []
 
     def allreduce_scalars(self, t: torch.Tensor):

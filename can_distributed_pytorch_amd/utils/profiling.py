@@ -14,7 +14,6 @@ import contextlib
 import ctypes
 import glob
 import os
-from collections import defaultdict
 
 import torch
 
@@ -62,24 +61,3 @@ def mark(name: str):
     lib = _load_roctx() if _enabled else None
     if lib:
         lib.roctxMarkA(name.encode())
-
-
-class CudaEventTimer:
-    """Accumulates device time per region name (hipEvent pairs, read lazily)."""
-
-    def __init__(self):
-        self.pending = defaultdict(list)
-
-    @contextlib.contextmanager
-    def region(self, name: str):
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        try:
-            yield
-        finally:
-            e.record()
-            self.pending[name].append((s, e))
-
-    def summary(self):
-        torch.cuda.synchronize()
-        return {k: sum(s.elapsed_time(e) for s, e in v) for k, v in self.pending.items()}

@@ -27,6 +27,7 @@ def main():
     from can_distributed_pytorch_amd.models import CANNet
     from can_distributed_pytorch_amd.ops.executor import CANNetExecutor
     from can_distributed_pytorch_amd.ops import conv as C
+    from can_distributed_pytorch_amd.ops import dispatch
     n, h, w = (int(v) for v in sys.argv[1:4]) if len(sys.argv) >= 4 else (8, 96, 128)
     c = 512
     torch.manual_seed(0)
@@ -40,29 +41,26 @@ def main():
     ws = C.WgradWorkspace(fv.device)
     gf = 2 * n * h * w * c * c * 4 / 1e9
     res = {}
-    for lin in ("1", "0"):
-        os.environ["CANNET_CTX_LINEAR"] = lin
-        tag = "linear" if lin == "1" else "direct"
-        res[f"{tag} fwd"] = timeit(lambda: ex._context_fwd(fv, True))
-        cat, sv = ex._context_fwd(fv, True)
-        res[f"{tag} bwd (main+side, serial)"] = timeit(
-            lambda: ex._context_bwd(sv, fv, dcat, grads, ws, 0.0, 1.0, lambda i: None))
-    os.environ["CANNET_CTX_LINEAR"] = "1"
+    for lin in (1, 0):
+        with dispatch.override(ctx_linear=lin):
+            tag = "linear" if lin == 1 else "direct"
+            res[f"{tag} fwd"] = timeit(lambda: ex._context_fwd(fv, True))
+            cat, sv = ex._context_fwd(fv, True)
+            res[f"{tag} bwd (main+side, serial)"] = timeit(
+                lambda: ex._context_bwd(sv, fv, dcat, grads, ws, 0.0, 1.0, lambda i: None))
     cat, sv = ex._context_fwd(fv, True)
     t = torch.randn(n, 50, c, device="cuda")
     u = torch.randn(n, 50, c, device="cuda")
     res["CTXF gemm"] = timeit(lambda: C.conv_ctx_fwd(fv, ex.ctx2cat_fwd, t, u))
-    os.environ["CANNET_CTX_TILEF"] = "128"
-    res["CTXF gemm 128x128 tiles"] = timeit(lambda: C.conv_ctx_fwd(fv, ex.ctx2cat_fwd, t, u))
-    os.environ.pop("CANNET_CTX_TILEF")
+    with dispatch.override(ctx_tile_f=128):
+        res["CTXF gemm 128x128 tiles"] = timeit(lambda: C.conv_ctx_fwd(fv, ex.ctx2cat_fwd, t, u))
     res["plain 1x1 gemm fv x W2cat (EPI_NONE)"] = timeit(lambda: C.conv_igemm(fv, ex.ctx2cat_fwd, None, ksize=1,
                                                                                  epi=C.EPI_NONE))
     dg, rowacc = C.ctx_bwd_lin(dcat, sv["wts"], sv["u"])
     res["ctx_bwd_lin"] = timeit(lambda: C.ctx_bwd_lin(dcat, sv["wts"], sv["u"]))
     res["CTXB gemm"] = timeit(lambda: C.conv_ctx_bwd(dg, ex.ctx2cat_dgr, t, dcat, fv))
-    os.environ["CANNET_CTX_TILEB"] = "128"
-    res["CTXB gemm 128x128 tiles"] = timeit(lambda: C.conv_ctx_bwd(dg, ex.ctx2cat_dgr, t, dcat, fv))
-    os.environ.pop("CANNET_CTX_TILEB")
+    with dispatch.override(ctx_tile_b=128):
+        res["CTXB gemm 128x128 tiles"] = timeit(lambda: C.conv_ctx_bwd(dg, ex.ctx2cat_dgr, t, dcat, fv))
     res["plain 1x1 gemm dG x W2cat^T (EPI_NONE)"] = timeit(lambda: C.conv_igemm(dg, ex.ctx2cat_dgr, None, ksize=1,
                                                                                    epi=C.EPI_NONE))
     dw = torch.empty(4 * c, c, 1, 1, device="cuda")

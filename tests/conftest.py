@@ -21,3 +21,17 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture
+def dispatch_cfg():
+    """Switch kernel-dispatch fields for one test (ops/dispatch.py); the previous config is restored after it.
+    ``dispatch_cfg(rring=0)`` — the only way a test selects a non-default variant (no environment variables)."""
+    import dataclasses
+    from can_distributed_pytorch_amd.ops import dispatch
+    prev = dispatch.current()
+
+    def set_(**kw):
+        dispatch.apply(dataclasses.replace(dispatch.current(), **kw))
+    yield set_
+    dispatch.apply(prev)

@@ -1,7 +1,7 @@
 """The native context module (model/CANNet.py:42-87) in isolation: forward (fv -> cat(fv, fi)) and backward
 (dcat -> d(F10 pre-activation), conv{S}_1 / conv{S}_2 weight gradients) of the executor against the fp32 autograd
 reference of the same math, for the linearised one-GEMM form (conv_igemm.hip EPI_CTXF / EPI_CTXB, default when
-the map is >= 64 columns wide) and the direct per-scale form (CANNET_CTX_LINEAR=0)."""
+the map is >= 64 columns wide) and the direct per-scale form (dispatch ctx_linear = 0)."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -29,11 +29,11 @@ def _ref_context(model, fv):
     return torch.cat((fv, num / (den + 1e-12)), 1)
 
 
-def _run(monkeypatch, linear, n, h, w, seed):
+def _run(dispatch_cfg, linear, n, h, w, seed):
     from can_distributed_pytorch_amd.models import CANNet
     from can_distributed_pytorch_amd.ops.executor import CANNetExecutor
     from can_distributed_pytorch_amd.ops import conv as C
-    monkeypatch.setenv("CANNET_CTX_LINEAR", "1" if linear else "0")
+    dispatch_cfg(ctx_linear=1 if linear else 0)
     torch.manual_seed(seed)
     model = CANNet(backend="hip").cuda()
     with torch.no_grad():
@@ -76,25 +76,24 @@ def _run(monkeypatch, linear, n, h, w, seed):
 
 @pytest.mark.parametrize("tile", ["256", "128"])
 @pytest.mark.parametrize("n,h,w", [(2, 17, 65), (1, 12, 128), (2, 9, 96)])
-def test_context_linear_vs_fp32(monkeypatch, n, h, w, tile):
-    monkeypatch.setenv("CANNET_CTX_TILEF", tile)
-    monkeypatch.setenv("CANNET_CTX_TILEB", tile)
-    e_fwd, e_dfv, e_w = _run(monkeypatch, True, n, h, w, seed=n * 100 + h)
+def test_context_linear_vs_fp32(dispatch_cfg, n, h, w, tile):
+    dispatch_cfg(ctx_tile_f=int(tile), ctx_tile_b=int(tile))
+    e_fwd, e_dfv, e_w = _run(dispatch_cfg, True, n, h, w, seed=n * 100 + h)
     assert e_fwd < 5e-3, e_fwd
     assert e_dfv < 2e-2, e_dfv
     assert all(v < 2e-2 for v in e_w.values()), e_w
 
 
 @pytest.mark.parametrize("n,h,w", [(2, 9, 12), (1, 12, 128)])
-def test_context_direct_vs_fp32(monkeypatch, n, h, w):
-    e_fwd, e_dfv, e_w = _run(monkeypatch, False, n, h, w, seed=7)
+def test_context_direct_vs_fp32(dispatch_cfg, n, h, w):
+    e_fwd, e_dfv, e_w = _run(dispatch_cfg, False, n, h, w, seed=7)
     assert e_fwd < 5e-3, e_fwd
     assert e_dfv < 2e-2, e_dfv
     assert all(v < 2e-2 for v in e_w.values()), e_w
 
 
-def test_context_linear_matches_direct(monkeypatch):
+def test_context_linear_matches_direct(dispatch_cfg):
     """Same inputs through both forms: the two bf16 implementations agree as closely as each agrees with fp32."""
-    a = _run(monkeypatch, True, 1, 12, 128, seed=3)
-    b = _run(monkeypatch, False, 1, 12, 128, seed=3)
+    a = _run(dispatch_cfg, True, 1, 12, 128, seed=3)
+    b = _run(dispatch_cfg, False, 1, 12, 128, seed=3)
     assert a[0] < 2 * b[0] + 1e-3 and a[1] < 2 * b[1] + 1e-3, (a, b)

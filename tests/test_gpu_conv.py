@@ -150,13 +150,13 @@ def test_conv_wgrad_first_layer():
 
 @pytest.mark.parametrize("ring", ["1", "0"])
 @pytest.mark.parametrize("n,h,w,ci,co", [(1, 256, 1024, 64, 64), (2, 181, 733, 128, 128), (1, 301, 900, 64, 128)])
-def test_conv_wgrad_halo_path(n, h, w, ci, co, ring, monkeypatch):
+def test_conv_wgrad_halo_path(n, h, w, ci, co, ring, dispatch_cfg):
     """Large-M, small-channel layers take the halo-tiled wgrad kernel (odd H, W not a multiple of 64 included).
     ring=1 (default): row-ring kernel, 4-row tiles down 64-column strips; the last two shapes have slices that
     cross strip boundaries (full-halo reload mid-slice) and a ragged last tile row."""
     from can_distributed_pytorch_amd.ops import _ext
     from can_distributed_pytorch_amd.ops import conv as C
-    monkeypatch.setenv("CANNET_WGRAD_RING", ring)
+    dispatch_cfg(wgrad_halo_ring=int(ring))
     assert _ext.require().wgrad_plan(n * h * w, ci, co, 3, 0, 1024)[2] == 8
     torch.manual_seed(5)
     x = torch.randn(n, h, w, ci, device="cuda").to(torch.bfloat16)
@@ -174,9 +174,9 @@ def test_conv_wgrad_halo_path(n, h, w, ci, co, ring, monkeypatch):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("n,h,w,ci,co", [(2, 128, 1024, 64, 64), (1, 512, 576, 128, 128), (4, 96, 704, 64, 128)])
-def test_ring_wgrad_fast_addressing_bitwise(n, h, w, ci, co, dtype, monkeypatch):
+def test_ring_wgrad_fast_addressing_bitwise(n, h, w, ci, co, dtype, dispatch_cfg):
     """Row-ring weight gradient with the hoisted DMA addressing (H % 4 == 0, W % 64 == 0: per-lane offsets from the
-    tile / row origins, edge slots zeroed per lane) == the general per-piece addressing (CANNET_RING_FAST=0),
+    tile / row origins, edge slots zeroed per lane) == the general per-piece addressing (ring_fast = 0),
     bitwise: several strips per image, several images, 2 ci / co tiles, slices crossing strips."""
     from can_distributed_pytorch_amd.ops import _ext
     from can_distributed_pytorch_amd.ops import conv as C
@@ -189,9 +189,9 @@ def test_ring_wgrad_fast_addressing_bitwise(n, h, w, ci, co, dtype, monkeypatch)
     ws = C.WgradWorkspace("cuda")
     C.conv_wgrad(dy, x, dw0, db0, ksize=3, dil=1, ws=ws)             # FAST + SKEW (default)
     dw2, db2 = torch.empty_like(dw0), torch.empty_like(db0)
-    monkeypatch.setenv("CANNET_RING_SKEW", "0")                        # FAST, every wave issues DMA
+    dispatch_cfg(ring_skew=0)                                          # FAST, every wave issues DMA
     C.conv_wgrad(dy, x, dw2, db2, ksize=3, dil=1, ws=ws)
-    monkeypatch.setenv("CANNET_RING_FAST", "0")
+    dispatch_cfg(ring_fast=0)
     C.conv_wgrad(dy, x, dw1, db1, ksize=3, dil=1, ws=ws)
     torch.cuda.synchronize()
     assert torch.equal(dw0, dw1) and torch.equal(db0, db1)
@@ -278,7 +278,7 @@ def test_conv_pool_fwd_fused(n, h, w, ci, co, dil, dtype):
 
 @pytest.mark.parametrize("n,h,w,ci,co,dil,beta", [(2, 8, 64, 512, 256, 2, 0.0), (1, 6, 128, 1024, 512, 1, 1.0),
                                                     (2, 5, 64, 256, 512, 2, 0.5)])
-def test_wgrad_tiled_reduction_matches_grid_stride(n, h, w, ci, co, dil, beta, monkeypatch):
+def test_wgrad_tiled_reduction_matches_grid_stride(n, h, w, ci, co, dil, beta, dispatch_cfg):
     """The LDS-transposing slab reduction (coalesced dW writes) == the grid-stride one, bitwise, beta included."""
     from can_distributed_pytorch_amd.ops import conv as C
     torch.manual_seed(11)
@@ -287,11 +287,8 @@ def test_wgrad_tiled_reduction_matches_grid_stride(n, h, w, ci, co, dil, beta, m
     dw0 = torch.randn(co, ci, 3, 3, device="cuda")
     db0 = torch.randn(co, device="cuda")
     out = []
-    for env in ("1", None):
-        if env:
-            monkeypatch.setenv("CANNET_REDUCE_GRIDSTRIDE", env)
-        else:
-            monkeypatch.delenv("CANNET_REDUCE_GRIDSTRIDE", raising=False)
+    for tiled in (0, 1):
+        dispatch_cfg(reduce_tiled=tiled)
         dw, db = dw0.clone(), db0.clone()
         C.conv_wgrad(dy, x, dw, db, ksize=3, dil=dil, beta=beta, scale=0.25)
         torch.cuda.synchronize()
@@ -326,42 +323,6 @@ def test_conv_dgrad_pool_backward_fused(n, h, w, ci, co, dtype):
     torch.cuda.synchronize()
     assert torch.equal(via_codes, ref)
     assert torch.equal(fused, ref)
-
-
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("n,h,w", [(2, 40, 136), (1, 301, 900)])
-def test_conv1_2_with_conv1_1_recomputed_is_bitwise_stored_path(n, h, w, dtype, monkeypatch):
-    """conv1_2 fwd / dgrad / wgrad with conv1_1's output recomputed from the image == the stored-X2 path, bitwise
-    (same MFMA K order for conv1_1, same rounding).  The stored-path weight gradient runs on the 2-row halo
-    kernel here (CANNET_WGRAD_RING=0): the recompute kernel shares its tile order, the row-ring kernel does not."""
-    from can_distributed_pytorch_amd.ops import conv as C
-    monkeypatch.setenv("CANNET_WGRAD_RING", "0")
-    torch.manual_seed(10)
-    img = torch.randn(n, 3, h, w, device="cuda")
-    x4 = C.to_nhwc4(img, dtype)
-    w1 = (torch.randn(64, 3, 3, 3, device="cuda") * 0.2).to(dtype).float()
-    b1 = torch.randn(64, device="cuda") * 0.1
-    w2 = (torch.randn(64, 64, 3, 3, device="cuda") * 0.05).to(dtype).float()
-    b2 = torch.randn(64, device="cuda") * 0.1
-    w1p = C.pack_weight_first(w1, dtype)
-    x2 = C.conv_igemm(x4, w1p, b1, ksize=3, first=True)
-    y_ref = C.conv_igemm(x2, C.pack_weight_fwd(w2, dtype), b2, ksize=3)
-    y = C.conv_f1(None, C.pack_weight_fwd(w2, dtype), b2, x4, w1p, b1, epi=C.EPI_BIAS_RELU)
-    assert torch.equal(y, y_ref)
-    dy = torch.randn(n, h, w, 64, device="cuda").to(dtype)
-    dx_ref = C.conv_igemm(dy, C.pack_weight_dgrad(w2, dtype), None, ksize=3, epi=C.EPI_MASK, mask=x2)
-    dx = C.conv_f1(dy, C.pack_weight_dgrad(w2, dtype), None, x4, w1p, b1, epi=C.EPI_MASK)
-    assert torch.equal(dx, dx_ref)
-    ws = C.WgradWorkspace("cuda")
-    dw_ref, db_ref = torch.empty(64, 64, 3, 3, device="cuda"), torch.empty(64, device="cuda")
-    dw, db = torch.empty_like(dw_ref), torch.empty_like(db_ref)
-    C.conv_wgrad(dy, x2, dw_ref, db_ref, ksize=3, ws=ws)
-    C.conv_wgrad_f1(dy, x4, w1p, b1, dw, db, ws=ws)
-    if n * h * w >= 262144:          # both on the halo kernel with the same slicing: bitwise
-        assert torch.equal(dw, dw_ref) and torch.equal(db, db_ref)
-    else:
-        _close(dw, dw_ref, 1e-3)
-        _close(db, db_ref, 1e-3)
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
@@ -409,9 +370,9 @@ def test_dgrad_bias_partials_feed_wgrad(n, h, w, ci, co, dil, epi, dtype):
 
 @pytest.mark.parametrize("epi", ["fwd", "bias", "none", "dgrad", "pool"])
 @pytest.mark.parametrize("n,h,w", [(2, 64, 640), (1, 61, 600), (3, 8, 1024), (1, 4, 64)])
-def test_ws64_matches_halo_kernel(n, h, w, epi, monkeypatch):
+def test_ws64_matches_halo_kernel(n, h, w, epi, dispatch_cfg):
     """Cin = Cout = 64 convs: the weight-stationary persistent kernel (several tiles per block, ragged tiles)
-    == the per-tile halo kernel (CANNET_WS64=0) bitwise — the same MFMA k order per output — and both == the
+    == the per-tile halo kernel (ws64 = 0) bitwise — the same MFMA k order per output — and both == the
     fp32 reference."""
     from can_distributed_pytorch_amd.ops import conv as C
     torch.manual_seed(13)
@@ -435,9 +396,9 @@ def test_ws64_matches_halo_kernel(n, h, w, epi, monkeypatch):
         y, yp, codes = C.conv_pool_fwd(x, C.pack_weight_fwd(wt), b, ksize=3, codes=True)
         return y, yp, codes
 
-    monkeypatch.setenv("CANNET_WS64", "1")
+    dispatch_cfg(ws64=1)
     new = run()
-    monkeypatch.setenv("CANNET_WS64", "0")
+    dispatch_cfg(ws64=0)
     old = run()
     torch.cuda.synchronize()
     for a_, b_ in zip(new, old):
@@ -502,68 +463,6 @@ def test_conv_dgrad_w1g_fused(n, h, w, beta, dtype):
     _close(db, db2, 5e-3)
 
 
-@pytest.mark.parametrize("ring", ["4", "5"])
-@pytest.mark.parametrize("n,h,w,ci,co,dil,k", [
-    (1, 6, 64, 256, 256, 1, 3), (2, 5, 128, 512, 256, 2, 3), (1, 3, 64, 1024, 512, 2, 3), (2, 7, 128, 512, 512, 1, 3),
-    (2, 4, 128, 512, 2048, 1, 1)])
-def test_wgrad_deep_ring_bitwise(n, h, w, ci, co, dil, k, ring, monkeypatch):
-    """v3 weight gradient (32-pixel stages in a 4- / 5-deep LDS-DMA ring, CANNET_WGRAD_RING) == v2 (two 64-pixel
-    stages) bitwise: the same MFMAs accumulate the same pixels in the same order per output element."""
-    from can_distributed_pytorch_amd.ops import conv as C
-    torch.manual_seed(31)
-    x = torch.randn(n, h, w, ci, device="cuda").to(torch.bfloat16)
-    dy = torch.randn(n, h, w, co, device="cuda").to(torch.bfloat16)
-    ws = C.WgradWorkspace("cuda")
-    dw0, db0 = torch.empty(co, ci, k, k, device="cuda"), torch.empty(co, device="cuda")
-    dw1, db1 = torch.empty_like(dw0), torch.empty_like(db0)
-    C.conv_wgrad(dy, x, dw0, db0, ksize=k, dil=dil, ws=ws)
-    monkeypatch.setenv("CANNET_WGRAD_RING", ring)
-    C.conv_wgrad(dy, x, dw1, db1, ksize=k, dil=dil, ws=ws)
-    torch.cuda.synchronize()
-    assert torch.equal(dw0, dw1) and torch.equal(db0, db1)
-
-
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("n,h,w,ci,co,k,dil", [(2, 8, 64, 256, 256, 3, 1), (1, 12, 16, 1024, 512, 3, 2),
-                                               (2, 16, 24, 512, 512, 1, 1), (1, 9, 13, 512, 256, 3, 2)])
-def test_glds_four_wave_tiles_bitwise(n, h, w, ci, co, k, dil, dtype, monkeypatch):
-    """256 x 256 tiles on 4 waves of 128 x 128 (CANNET_GLDS_W4=1, cfg 26) == the 8-wave layout (cfg 21), bitwise,
-    for every epilogue the default dispatch routes there: bias + ReLU, pool-fused forward, ReLU-mask data gradient
-    with bias partials, pool-backward data gradient, plain (same K order per output, same rounding)."""
-    from can_distributed_pytorch_amd.ops import conv as C
-    torch.manual_seed(31)
-    x = torch.randn(n, h, w, ci, device="cuda").to(dtype)
-    wt = (torch.randn(co, ci, k, k, device="cuda") * (2.0 / (k * k * ci)) ** 0.5).to(dtype).float()
-    b = torch.randn(co, device="cuda") * 0.1
-    wf = C.pack_weight_fwd(wt, dtype)
-    wdt = (torch.randn(ci, co, k, k, device="cuda") * 0.05).to(dtype).float()     # a co -> ci layer: dgrad ci -> co
-    wd = C.pack_weight_dgrad(wdt, dtype)
-    dy = torch.randn(n, h, w, ci, device="cuda").to(dtype)
-    mask = torch.randn(n, h, w, co, device="cuda").to(dtype)
-    full = torch.relu(torch.randn(n, 2 * h, 2 * w, co, device="cuda")).to(dtype)
-    full[:, ::3, ::2] = 0
-    _, codes = C.maxpool_codes(full)
-
-    def run():
-        r = [C.conv_igemm(x, wf, b, ksize=k, dil=dil),
-             C.conv_igemm(x, wf, None, ksize=k, dil=dil, epi=C.EPI_NONE)]
-        r += list(C.conv_dgrad_with_bias(dy, wd, ksize=k, dil=dil, epi=C.EPI_MASK, mask=mask))
-        if k == 3:
-            r += list(C.conv_dgrad_with_bias(dy, wd, ksize=3, dil=dil, epi=C.EPI_POOLBWD, mask=codes))
-        if C.conv_pool_fwd_ok(x, co, k):
-            r += list(C.conv_pool_fwd(x, wf, b, ksize=k, dil=dil, codes=True))
-        torch.cuda.synchronize()
-        return r
-
-    monkeypatch.delenv("CANNET_GLDS_W4", raising=False)
-    ref = run()
-    monkeypatch.setenv("CANNET_GLDS_W4", "1")
-    got = run()
-    assert len(got) == len(ref)
-    for g, r in zip(got, ref):
-        assert g is not None and torch.equal(g, r)
-
-
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("n,h,w,ci,co,dil", [(2, 8, 128, 256, 256, 1), (1, 12, 128, 1024, 512, 2),
                                              (1, 6, 256, 128, 256, 1), (2, 10, 384, 64, 256, 2),
@@ -572,9 +471,9 @@ def test_glds_four_wave_tiles_bitwise(n, h, w, ci, co, k, dil, dtype, monkeypatc
                                              (2, 8, 128, 128, 64, 1), (1, 8, 512, 128, 64, 1), (1, 4, 256, 256, 64, 2),
                                              # cfg 29: 128-channel 2-row tiles (the wave tile of cfg 22)
                                              (2, 6, 128, 256, 128, 1), (1, 4, 256, 384, 128, 2)])
-def test_row_ring_conv_bitwise(n, h, w, ci, co, dil, dtype, monkeypatch):
+def test_row_ring_conv_bitwise(n, h, w, ci, co, dil, dtype, dispatch_cfg):
     """Row-ring 3x3 conv (cfg 27 / 28: activation rows staged once per 64-channel chunk, taps read shifted windows
-    of the row slots) == the LDS-DMA kernel of the same tile (cfg 21 256 x 256 / cfg 23 64 x 512, CANNET_RRING=0)
+    of the row slots) == the LDS-DMA kernel of the same tile (cfg 21 256 x 256 / cfg 23 64 x 512, rring = 0)
     bitwise for every epilogue it takes:
     bias + ReLU, plain, bias, ReLU-mask data gradient with bias partials, pool-backward data gradient, fp32 store;
     one- and multi-block-wide maps (zero guards / neighbour-pixel guards), dilation 1 and 2, top/bottom padding."""
@@ -606,11 +505,9 @@ def test_row_ring_conv_bitwise(n, h, w, ci, co, dil, dtype, monkeypatch):
         torch.cuda.synchronize()
         return r
 
-    monkeypatch.setenv("CANNET_RRING", "0")
+    dispatch_cfg(rring=0)
     ref = run()
-    monkeypatch.setenv("CANNET_RRING", "2")          # every dilation
-    monkeypatch.setenv("CANNET_RRING64", "1")        # and the 64-channel 4-row tiles
-    monkeypatch.setenv("CANNET_RRING128", "3")       # and the 128-channel 2-row tiles (every K, every dilation)
+    dispatch_cfg(rring=2, rring64=1, rring128=3)   # every dilation, 64-channel 4-row and 128-channel 2-row tiles
     got = run()
     assert len(got) == len(ref)
     for i, (g, r) in enumerate(zip(got, ref)):

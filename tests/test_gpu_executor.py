@@ -171,54 +171,8 @@ def test_batched_packs_match_reference_packing():
         assert torch.equal(dgr, C.pack_weight_dgrad(w))
 
 
-def test_native_stepper_f1_recompute_matches_stored(monkeypatch):
-    """conv1_1 recomputed inside conv1_2's kernels (CANNET_F1_FUSED=1) trains like the stored path."""
-    from can_distributed_pytorch_amd.engine.native import NativeStepper
-    _, nat_a = _models(6)
-    nat_b = copy.deepcopy(nat_a)
-    init = [(n, p.detach().clone()) for n, p in nat_a.named_parameters()]
-    x = torch.randn(2, 3, 64, 128, device="cuda")
-    gt = torch.rand(2, 1, 8, 16, device="cuda")
-    a = NativeStepper("cuda", lr=1e-7, graph=False, model=nat_a)
-    b = NativeStepper("cuda", lr=1e-7, graph=False, model=nat_b)
-    la, lb = [], []
-    for _ in range(3):
-        monkeypatch.setenv("CANNET_F1_FUSED", "0")
-        la.append(float(a.step(x, gt)))
-        monkeypatch.setenv("CANNET_F1_FUSED", "1")
-        lb.append(float(b.step(x, gt)))
-    torch.cuda.synchronize()
-    assert b.ex._f1_fused()
-    for u, v in zip(la, lb):
-        assert abs(u - v) <= 1e-3 * abs(u), (la, lb)
-    for (name, p0), pa, pb in zip(init, nat_a.parameters(), nat_b.parameters()):
-        assert _rel(pb - p0, pa - p0) < 2e-2, name    # the updates, not the weights
-
-
-def test_native_stepper_f0_wgrad_on_compute_stream_bitwise(monkeypatch):
-    """conv1_1's weight gradient on the compute stream (CANNET_F0_WGRAD_MAIN=1, own slab workspace) gives the
-    same weights, bit for bit, as the default schedule on the weight-gradient stream."""
-    from can_distributed_pytorch_amd.engine.native import NativeStepper
-    _, nat_a = _models(8)
-    nat_b = copy.deepcopy(nat_a)
-    x = torch.randn(2, 3, 96, 128, device="cuda")
-    gt = torch.rand(2, 1, 12, 16, device="cuda")
-    monkeypatch.setenv("CANNET_W1G", "0")                # conv1_1's separate weight-gradient launch
-    a = NativeStepper("cuda", lr=1e-4, graph=False, model=nat_a)
-    b = NativeStepper("cuda", lr=1e-4, graph=False, model=nat_b)
-    for _ in range(3):
-        monkeypatch.setenv("CANNET_F0_WGRAD_MAIN", "0")
-        a.step(x, gt)
-        monkeypatch.setenv("CANNET_F0_WGRAD_MAIN", "1")
-        b.step(x, gt)
-    torch.cuda.synchronize()
-    assert b.ex.ws_main is not None
-    for (name, pa), pb in zip(nat_a.named_parameters(), nat_b.parameters()):
-        assert torch.equal(pa, pb), name
-
-
-def test_native_stepper_w1g_fused_matches_default(monkeypatch):
-    """conv1_1's weight gradient fused into conv1_2's data gradient (CANNET_W1G=1, the default) trains like the separate-launch
+def test_native_stepper_w1g_fused_matches_default(dispatch_cfg):
+    """conv1_1's weight gradient fused into conv1_2's data gradient (dispatch w1g = 1, the default) trains like the separate-launch
     schedule (same kernels elsewhere; the fused product sums in a different order)."""
     from can_distributed_pytorch_amd.engine.native import NativeStepper
     _, nat_a = _models(9)
@@ -230,9 +184,9 @@ def test_native_stepper_w1g_fused_matches_default(monkeypatch):
     b = NativeStepper("cuda", lr=1e-7, graph=False, model=nat_b)
     la, lb = [], []
     for _ in range(3):
-        monkeypatch.setenv("CANNET_W1G", "0")
+        dispatch_cfg(w1g=0)
         la.append(float(a.step(x, gt)))
-        monkeypatch.setenv("CANNET_W1G", "1")
+        dispatch_cfg(w1g=1)
         lb.append(float(b.step(x, gt)))
     torch.cuda.synchronize()
     assert b.ex._w1g_buf is not None
@@ -258,9 +212,9 @@ def test_rccl_comm_init_is_bounded_when_a_peer_never_joins():
 
 
 @pytest.mark.parametrize("mode", ["1", "2"])
-def test_native_stepper_row_ring_matches_per_tap_kernel(mode, monkeypatch):
-    """The row-ring conv (cfg 27: dilation-1 layers by default, every dilation with CANNET_RRING=2) trains exactly
-    like the per-tap LDS-DMA kernel (CANNET_RRING=0): 1 x 64 x 1024 puts conv3_x on a 2-block-wide 256-column map
+def test_native_stepper_row_ring_matches_per_tap_kernel(mode, dispatch_cfg):
+    """The row-ring conv (cfg 27: dilation-1 layers by default, every dilation with rring = 2) trains exactly
+    like the per-tap LDS-DMA kernel (rring = 0): 1 x 64 x 1024 puts conv3_x on a 2-block-wide 256-column map
     (neighbour-pixel guards), conv4_x and the backend on a 1-block-wide 128-column map (zero guards).  Weights match
     bit for bit after a step; biases to rounding (a 2-block-wide map groups the epilogue's bias partials by 2 x 128
     tiles instead of 256-pixel runs)."""
@@ -269,11 +223,10 @@ def test_native_stepper_row_ring_matches_per_tap_kernel(mode, monkeypatch):
     nat_b = copy.deepcopy(nat_a)
     x = torch.randn(1, 3, 64, 1024, device="cuda")
     gt = torch.rand(1, 1, 8, 128, device="cuda")
-    monkeypatch.setenv("CANNET_RRING", "0")
+    dispatch_cfg(rring=0)
     a = NativeStepper("cuda", lr=1e-4, graph=False, model=nat_a)
     a.step(x, gt)
-    monkeypatch.setenv("CANNET_RRING", mode)
-    monkeypatch.setenv("CANNET_RRING64", "1")
+    dispatch_cfg(rring=int(mode), rring64=1)
     b = NativeStepper("cuda", lr=1e-4, graph=False, model=nat_b)
     b.step(x, gt)
     torch.cuda.synchronize()
