@@ -155,7 +155,11 @@ def build(jobs: int = 8, verbose: bool = False, asan: bool = False) -> str:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
-            # python symbols are resolved at import time; retry without --no-undefined
+            # python symbols are resolved at import time; retry without --no-undefined, but never with an undefined
+            # symbol of our own (can_* / can::): that would only surface as an import error on the GPU box
+            import re
+            if re.search(r"undefined reference to `[^']*can_", r.stderr):
+                raise RuntimeError(f"link failed: undefined extension symbol\n{r.stderr[-4000:]}")
             cmd = [c for c in cmd if c != "-Wl,--no-undefined"]
             r = subprocess.run(cmd, capture_output=True, text=True)
             if r.returncode != 0:

@@ -95,6 +95,8 @@ int can_synth_render(const float* dens, const float* noise, float* dmax, void* x
 int can_preprocess_density(const float* d, int H0, int W0, int flip, float* out, int Ho, int Wo, float mult,
                            void* stream);
 
+int can_conv_plan(int H, int W, int Cin, int Cout, int ksize, int dil, int epi);
+
 #ifdef __cplusplus
 }
 #endif

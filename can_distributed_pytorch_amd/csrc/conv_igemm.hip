@@ -333,17 +333,22 @@ struct ConvArgs2 {
   const bf16_t* fvp = nullptr;
   int cC = 0;
   int ctx_prologue = 0;    // 1: the launch reserved LDS for the row tables beside the staging ring
+  // row-ring kernel (conv_rring_kernel): 128-column blocks per image row (ceil(W / 128)), RT-row tile rows per image
+  // (ceil(H / RT)) and the pixel-tile count N * rr_ty * rr_tx; a ragged last block / tile row is masked
+  int rr_tx = 0, rr_ty = 0, rr_np = 0;
 };
 
 // pixel m of row r of pixel tile pt; EPI_POOLFWD tiles are 2 rows x TP/2 columns, rows interleaved per
 // 16-pixel fragment (see EPI_POOLFWD), the other epilogues take TP consecutive pixels
 // RT (row-ring kernel, conv_rring_kernel): a tile is RT image rows x 128 columns, tile pt = (n, row group, 128-column
-// block) with the column block fastest; r = row * 128 + column (W % 128 == 0, H % RT == 0)
+// block) with the column block fastest; r = row * 128 + column.  Pixels of a ragged last column block (W % 128 != 0)
+// or tile row (H % RT != 0) map to a.M (= skipped by the epilogue)
 template <int TP, int EPI, int RT = 0>
 __device__ __forceinline__ int tile_pix(const ConvArgs2& a, int pt, int r) {
   if constexpr (RT != 0 && EPI != EPI_POOLFWD) {
-    const int tx = a.W >> 7, q = pt / tx, cb = pt - q * tx;
-    return (RT * q + (r >> 7)) * a.W + cb * 128 + (r & 127);
+    const int tx = a.rr_tx, q = pt / tx, cb = pt - q * tx;
+    const int n = q / a.rr_ty, oh = RT * (q - n * a.rr_ty) + (r >> 7), ow = cb * 128 + (r & 127);
+    return (oh < a.H && ow < a.W) ? (n * a.H + oh) * a.W + ow : a.M;
   } else if constexpr (EPI == EPI_POOLFWD) {
     const int ncb = a.W / (TP / 2);
     const int rp = pt / ncb, cb = pt - rp * ncb;    // rp = n * H/2 + pooled row
@@ -1189,7 +1194,8 @@ static int launch_glds2(const ConvArgs2& a, hipStream_t s, int nb = 1) {
 // ===========================================================================
 // Row-ring 3x3 conv (forward / data gradient; cfg 27): the 256 x 256 tile of conv_glds2 (8 waves of 64 channels x
 // 128 pixels, same MFMA order, same epilogue) with the activation operand staged once per input ROW instead of once
-// per tap.  A pixel tile is 2 image rows x 128 columns (W % 128 == 0, H even); for one 64-channel chunk its 9 taps
+// per tap.  A pixel tile is 2 image rows x 128 columns (a ragged last column block / tile row is masked: its DMA
+// reads the zero page, its epilogue skips the pixels); for one 64-channel chunk its 9 taps
 // read only 2 + 2 * dil input rows, each a 128-column row plus an 8-pixel guard on both sides.  The rows sit in a
 // 4-slot LDS ring (18 KB each) beside the 2-stage weight ring: a row is DMA'd two stages ahead of its first tap
 // (with that stage's weights) into the slot of the row whose last tap is already in registers, and every tap reads
@@ -1232,15 +1238,18 @@ __global__ void __launch_bounds__(512, 1) conv_rring_kernel(ConvArgs2 a) {
   const int rt = wp / WPR;                           // the tile row this wave computes
   const int cbw = (wp - rt * WPR) * 64 * PW;         // and its first column in the tile
 
-  const int tx = a.W >> 7;
+  const int tx = a.rr_tx;                                     // ceil(W / 128) column blocks
   const int nct = a.Cout / TC;
-  const int npt = a.M / TP;
+  const int npt = a.rr_np;
   const int tile = xcd_remap(blockIdx.x, nct * npt);
   const int ct = tile % nct, pt = tile / nct;
   const int q = pt / tx, cb = pt - q * tx;
-  const int grow0 = TR * q;                                   // n * H + oh0
-  const int oh0 = grow0 - (int)fdiv((uint32_t)grow0, a.fdH) * a.H;
+  const int nimg = q / a.rr_ty;
+  const int oh0 = TR * (q - nimg * a.rr_ty);
+  const int grow0 = nimg * a.H + oh0;                         // n * H + oh0
   const int col0 = cb * 128;
+  // a ragged last column block (W % 128 != 0): interior / guard pixels at or beyond W come from the zero page
+  const bool ragged_w = (a.W & 127) != 0;
   const int Ktot = 9 * a.Cin;
   const int nc = a.Cin >> 6, nk = 9 * nc;
   const int lc8 = ((lane & 7) ^ (lane >> 3)) * 8;             // swizzled 16-B chunk (pieces are 8-pixel aligned)
@@ -1298,12 +1307,14 @@ __global__ void __launch_bounds__(512, 1) conv_rring_kernel(ConvArgs2 a) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int j = wave + NW * h;                           // interior piece: pixels 8j .. 8j + 7
-        glds16(rv ? (const void*)(a.x + rbase + (size_t)(8 * j) * a.Cin + boff) : (const void*)(a.zero + lane * 8),
+        const bool cv = !ragged_w || col0 + 8 * j + (lane >> 3) < a.W;
+        glds16((rv && cv) ? (const void*)(a.x + rbase + (size_t)(8 * j) * a.Cin + boff)
+                          : (const void*)(a.zero + lane * 8),
                lds_addr(slot + (j + 1) * 1024));
       }
       if (tx > 1 && wave < 2) {
         // 8-pixel guards of an interior column block: real pixels of the neighbouring blocks (wave 0 left, 1 right)
-        const bool gv = rv && (wave == 0 ? cb > 0 : cb + 1 < tx);
+        const bool gv = rv && (wave == 0 ? cb > 0 : (cb + 1 < tx && (!ragged_w || col0 + 128 + (lane >> 3) < a.W)));
         const long long gc = (wave == 0) ? -8 : 128;
         glds16(gv ? (const void*)(a.x + (long long)rbase + gc * a.Cin + boff) : (const void*)(a.zero + lane * 8),
                lds_addr(slot + (wave == 0 ? 0 : 17) * 1024));
@@ -1412,22 +1423,33 @@ __global__ void __launch_bounds__(512, 1) conv_rring_kernel(ConvArgs2 a) {
   glds_epilogue<DT, WC, WP, PW, EPI, TR>(a, acc, ct, pt, wc, wp, fr, fq);
 }
 
-// the row-ring kernel applies: 3x3, dilation 1 / 2, W % 128 == 0; Cout % 256 == 0 with H even (cfg 27) or Cout == 64
-// with H % 4 == 0 (cfg 28); 0 = not applicable
+// column-block utilisation of the row ring on a ragged width: W / (ceil(W / 128) * 128) >= 0.7 (W = 240, 480,
+// 960: 94 %); below it (W = 135: 53 %) the per-tap LDS-DMA kernel, whose pixel tiles run across rows, wastes less
+static bool rring_width_ok(int W) {
+  if (W % 128 == 0) return true;
+  const int tx = (W + 127) / 128;
+  return W >= 96 && 10 * W >= 7 * 128 * tx;
+}
+// pixel tiles of the row ring: N * ceil(H / TR) * ceil(W / 128) (ragged last tile row / column block masked)
+static int rr_np(int H, int W, int M, int TR) {
+  return (M / (H * W)) * ((H + TR - 1) / TR) * ((W + 127) / 128);
+}
+// the row-ring kernel applies: 3x3, dilation 1 / 2, a width the column blocks cover well (rring_width_ok); Cout % 256
+// == 0 (cfg 27, 2-row tiles), Cout % 128 (cfg 29) or Cout == 64 (cfg 28, 4-row tiles); 0 = not applicable
 static int rring_cfg(int H, int W, int Cin, int Cout, int ksize, int dil, int epi) {
-  if (ksize != 3 || (dil != 1 && dil != 2) || W % 128 || Cin % 64 || epi == EPI_POOLFWD || epi == EPI_SIGMOID ||
-      epi == EPI_CTXF || epi == EPI_CTXB)
+  if (ksize != 3 || (dil != 1 && dil != 2) || !rring_width_ok(W) || Cin % 64 || epi == EPI_POOLFWD ||
+      epi == EPI_SIGMOID || epi == EPI_CTXF || epi == EPI_CTXB)
     return 0;
-  if (Cout % 256 == 0 && H % 2 == 0) return 27;
+  if (Cout % 256 == 0) return 27;
   // cfg 29 (128 x (2 x 128), the wave tile of cfg 22): dispatch rring128 = 1 (default) for the dilation-1 cfg-22
   // layers (K > 1152: conv3_1's data gradient 0.270 -> 0.253 ms), = 2 also for the cfg-25 ones (128 x 512 tiles,
   // K <= 1152: conv2_2 +2 %), = 3 also dilation 2 (backend.8 forward +10 %); 0 = off (profiles/r3/ab_rring128.txt)
   const int m128 = g_dispatch.rring128;
-  if (Cout % 128 == 0 && Cout % 256 != 0 && H % 2 == 0 && m128 >= ((9 * Cin > 1152) ? 1 : 2) && (dil == 1 || m128 >= 3))
+  if (Cout % 128 == 0 && Cout % 256 != 0 && m128 >= ((9 * Cin > 1152) ? 1 : 2) && (dil == 1 || m128 >= 3))
     return 29;
   // cfg 28 (dispatch rring64 = 0: off): conv2_1's data gradient 0.435 -> 0.347 ms isolated, step 487.3 -> 489.9
   // img/s (profiles/r3/ab_dma_order.txt)
-  if (Cout == 64 && H % 4 == 0 && g_dispatch.rring64) return 28;
+  if (Cout == 64 && g_dispatch.rring64) return 28;
   return 0;
 }
 // dispatch rring: 0 = off, 1 = dilation-1 layers, 2 (default) = every dilation.  With the after-group DMA placement
@@ -1446,7 +1468,11 @@ static int launch_rring_one(const ConvArgs2& a, hipStream_t s) {
     CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, rr_lds(TC, TR)));
     attr = true;
   }
-  hipLaunchKernelGGL(kfn, dim3((a.Cout / TC) * (a.M / (128 * TR))), dim3(512), rr_lds(TC, TR), s, a);
+  ConvArgs2 b = a;
+  b.rr_tx = (a.W + 127) / 128;
+  b.rr_ty = (a.H + TR - 1) / TR;
+  b.rr_np = rr_np(a.H, a.W, a.M, TR);
+  hipLaunchKernelGGL(kfn, dim3((a.Cout / TC) * b.rr_np), dim3(512), rr_lds(TC, TR), s, b);
   return (int)hipGetLastError();
 }
 
@@ -2178,13 +2204,17 @@ static int glds_default_cfg(int Cin, int Cout, int ksize) {
 static int glds_cfg_tp(int cfg) {   // pixels per tile of a v2 config
   return (cfg == 21 || cfg == 22) ? 256 : (cfg == 23 || cfg == 25) ? 512 : 0;
 }
-// rows of the bias-partial matrix an LDS-DMA config writes: pixel tiles x waves along the pixels (0: none)
-static int glds_bpart_rows(int cfg, int M) {
+// rows of the bias-partial matrix an LDS-DMA config writes: pixel tiles x waves along the pixels (0: none); the
+// row ring's pixel tiles are per-image row groups x column blocks (rr_np)
+static int glds_bpart_rows(int cfg, int M, int H, int W) {
   int tp = 0, wp = 0;
   switch (cfg) {
-    case 11: case 21: case 27: tp = 256; wp = 2; break;   // 256 ch x 256 px, 4 x 2 waves
-    case 12: case 22: case 29: tp = 256; wp = 4; break;   // 128 x 256, 2 x 4
-    case 13: case 23: case 28: tp = 512; wp = 8; break;   // 64 x 512, 1 x 8
+    case 27: return rr_np(H, W, M, 2) * 2;     // 256 ch x (2 x 128) px, 4 x 2 waves
+    case 29: return rr_np(H, W, M, 2) * 4;     // 128 x (2 x 128), 2 x 4
+    case 28: return rr_np(H, W, M, 4) * 8;     // 64 x (4 x 128), 1 x 8
+    case 11: case 21: tp = 256; wp = 2; break;   // 256 ch x 256 px, 4 x 2 waves
+    case 12: case 22: tp = 256; wp = 4; break;   // 128 x 256, 2 x 4
+    case 13: case 23: tp = 512; wp = 8; break;   // 64 x 512, 1 x 8
     case 25: tp = 512; wp = 4; break;            // 128 x 512, 2 x 4 (2 fragments per wave)
     default: return 0;
   }
@@ -2297,7 +2327,7 @@ static int conv_igemm_impl(const void* x, const void* w, const float* bias, cons
     b.H = H; b.W = W; b.Cin = Cin; b.Cout = Cout; b.ksize = ksize; b.dil = dil; b.M = a.M;
     if (tile_cfg == 0 && rring_mode() >= dil) tile_cfg = rring_cfg(H, W, Cin, Cout, ksize, dil, epi);
     if (bpart != nullptr) {
-      const int rows = glds_bpart_rows(tile_cfg ? tile_cfg : glds_default_cfg(Cin, Cout, ksize), a.M);
+      const int rows = glds_bpart_rows(tile_cfg ? tile_cfg : glds_default_cfg(Cin, Cout, ksize), a.M, H, W);
       if (rows > 0 && rows <= bpart_cap) { b.bpart = bpart; if (bpart_rows) *bpart_rows = rows; }
     }
     b.fdW = make_fastdiv((uint32_t)W); b.fdH = make_fastdiv((uint32_t)H);
@@ -2459,6 +2489,17 @@ extern "C" int can_conv_pool_fwd(const void* x, const void* w, const float* bias
                                  void* stream) {
   CAN_DT_DISPATCH(dt, can::conv_pool_fwd_impl<DT>(x, w, bias, y, yp, codes, N, H, W, Cin, Cout, ksize, dil, tile_cfg,
                                               (hipStream_t)stream));
+}
+
+// the kernel configuration conv_igemm picks for a (non-first-layer) conv with tile_cfg 0: 31 = halo kernel (Cin = 64),
+// 33 = its weight-stationary ws64 form (Cin = Cout = 64), 27 / 28 / 29 = row ring, else the LDS-DMA tile config
+extern "C" int can_conv_plan(int H, int W, int Cin, int Cout, int ksize, int dil, int epi) {
+  using namespace can;
+  if (Cin == 64 && ksize == 3 && dil == 1 && (Cout == 64 || Cout == 128) && epi != EPI_SIGMOID &&
+      epi != EPI_POOLBWD && epi != EPI_F32)
+    return (Cout == 64 && use_ws64()) ? 33 : 31;
+  const int rr = (rring_mode() >= dil) ? rring_cfg(H, W, Cin, Cout, ksize, dil, epi) : 0;
+  return rr ? rr : glds_default_cfg(Cin, Cout, ksize);
 }
 
 // pixels per tile of the kernel conv_pool_fwd runs for this layer (tile_cfg 0 = default): the fused pool

@@ -304,6 +304,12 @@ struct WgradArgs2 {
   // operands nb apart by these element strides, slabs by S*K*Cout (default 1 / 0)
   int nb = 1;
   long long dy_bs = 0, x_bs = 0;
+  // wgrad_glds2 on a ragged width (W % 64 != 0): the pixel index is VIRTUAL — every image row padded to
+  // tx64 = ceil(W / 64) 64-pixel stages (M, mslice count virtual pixels); the padding pixels' activations come from
+  // the zero page, so they add nothing.  tx64 = W / 64 and fdTX = fdiv by it on an aligned width (the same stages)
+  int tx64 = 0;
+  FastDiv fdTX;
+  int Mreal = 0;        // real pixel count (the dY descriptor's range); M is virtual on a ragged width
 };
 
 template <int RB>   // row bytes
@@ -546,7 +552,7 @@ static int launch_wgrad2(const WgradArgs2& a, hipStream_t s) {
 // first half's MFMAs, the next stage's first half read right after the
 // barrier under the other half).
 // ===========================================================================
-template <int DT, int WC, int WK, int KW>
+template <int DT, int WC, int WK, int KW, bool RW = false>
 __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2 a) {
   constexpr int NW = WC * WK;
   constexpr int TCo = 64 * WC, TK = 64 * WK * KW;
@@ -580,13 +586,15 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
   // per-lane base offset + a wave-uniform stride per piece replaces the per-piece offset arrays (they
   // pushed this kernel to 256 VGPRs with spills)
   const __amdgpu_buffer_rsrc_t dy_rsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)gdy, (short)0, a.M * a.Cout * 2, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)gdy, (short)0, a.Mreal * a.Cout * 2, 0x00020000);
   constexpr int ASTEP = NW * 1024 / RBA, BSTEP = NW * 1024 / RBB;    // rows between pieces
   static_assert(ASTEP % 16 == 0 && BSTEP % 16 == 0, "piece stride must keep the row swizzle");
   unsigned aoff0;
+  int arow0;
   {
     const int byte = wave * 1024 + lane * 16;
     const int row = byte / RBA;
+    arow0 = row;
     const int lc16 = swz8b<RBA>(row, ((byte % RBA) / 16) * 2) >> 1;
     aoff0 = (unsigned)(row * a.Cout + co0 + lc16 * 8) * 2u;
   }
@@ -623,9 +631,10 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
   };
   auto stage_addr = [&](int st, int buf) -> StageAddr {
     StageAddr sa;
-    const int m0 = mbeg + st * BKM;
-    const uint32_t q = fdiv((uint32_t)m0, a.fdW);
-    sa.ow0 = m0 - (int)q * a.W;
+    const int g = (mbeg + st * BKM) >> 6;             // virtual 64-pixel stage = (image row q, column block)
+    const uint32_t q = fdiv((uint32_t)g, a.fdTX);
+    sa.ow0 = (g - (int)q * a.tx64) * 64;
+    const int m0 = (int)q * a.W + sa.ow0;             // its first real pixel
     const int oh = (int)q - (int)fdiv(q, a.fdH) * a.H;
     sa.row_ok = (unsigned)(oh + dh) < (unsigned)a.H;     // stage-uniform
     sa.sbase = smem + buf * STAGE;
@@ -638,12 +647,23 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
     return;                                         // diagnostic build (scripts/probe): no DMA
 #endif
 #pragma unroll
-    for (int j = p * GA / parts; j < (p + 1) * GA / parts; ++j)
-      blds16(dy_rsrc, aoff0 + j * astride, sa.soff, lds_addr(sa.sbase + (wave + NW * j) * 1024));
+    for (int j = p * GA / parts; j < (p + 1) * GA / parts; ++j) {
+      if constexpr (RW) {
+        // ragged width: the stage's padding pixels (>= W) are pixels of the next row (or past the end of dY): their
+        // lanes get an offset beyond the descriptor's range (the range check on the per-lane offset returns zeros);
+        // the stage base travels in the per-lane offset, not in soffset
+        const bool okA = sa.ow0 + arow0 + j * ASTEP < a.W;
+        blds16(dy_rsrc, okA ? aoff0 + j * astride + sa.soff : 0xFFFFFFF0u, 0u,
+               lds_addr(sa.sbase + (wave + NW * j) * 1024));
+      } else {
+        blds16(dy_rsrc, aoff0 + j * astride, sa.soff, lds_addr(sa.sbase + (wave + NW * j) * 1024));
+      }
+    }
 #pragma unroll
     for (int j = p * GB / parts; j < (p + 1) * GB / parts; ++j) {
-      const int iw = sa.ow0 + dw + brow0 + j * BSTEP;
-      const bool ok = sa.row_ok && ((unsigned)iw < (unsigned)a.W);
+      const int ow = sa.ow0 + brow0 + j * BSTEP;      // this piece row's output pixel (>= W: ragged padding)
+      const int iw = ow + dw;
+      const bool ok = sa.row_ok && ((unsigned)iw < (unsigned)a.W) && ow < a.W;
       const void* src = ok ? (const void*)(sa.xs + boff0 + j * bstride) : (const void*)a.zero;
       glds16(src, lds_addr(sa.sbase + A_BYTES + (wave + NW * j) * 1024));
     }
@@ -815,11 +835,11 @@ __global__ void __launch_bounds__(256) bias_colsum_kernel(const bf16_t* __restri
   }
 }
 
-template <int DT, int WC, int WK, int KW>
+template <int DT, int WC, int WK, int KW, bool RW = false>
 static int launch_wgrad3(const WgradArgs2& a, hipStream_t s) {
   constexpr int STAGE = 64 * (64 * WC + 64 * WK * KW) * 2;
   const size_t lds = 2 * (size_t)STAGE;
-  auto kfn = wgrad_glds2_kernel<DT, WC, WK, KW>;
+  auto kfn = wgrad_glds2_kernel<DT, WC, WK, KW, RW>;
   static bool attr = false;
   if (!attr) {
     CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -1368,6 +1388,15 @@ static int conv_wgrad_impl(const void* dy, const void* x, float* ws, float* wsb,
     a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.ksize = ksize; a.dil = dil; a.M = N * H * W; a.K = K;
     a.S = S; a.mslice = mslice;
     a.fdW = make_fastdiv((uint32_t)W); a.fdH = make_fastdiv((uint32_t)H); a.fdC = make_fastdiv((uint32_t)Cin);
+    a.Mreal = a.M;
+    a.tx64 = (W + 63) / 64; a.fdTX = make_fastdiv((uint32_t)a.tx64);
+    // v2 on a ragged width: virtual pixels (every row padded to whole 64-pixel stages), the same slice count
+    const bool rw = (W % 64) != 0 && ksize == 3;
+    WgradArgs2 gv = a;
+    if (rw) {
+      gv.M = N * H * a.tx64 * 64;
+      gv.mslice = ((gv.M + S - 1) / S + 63) / 64 * 64;   // slices past the end run no stage and write zero slabs
+    }
     if (cfg == 8) {
       if (ksize != 3 || dil != 1 || (Cout != 64 && Cout != 128) || Cin % 64) return -6;
       HaloArgs h;
@@ -1396,15 +1425,15 @@ static int conv_wgrad_impl(const void* dy, const void* x, float* ws, float* wsb,
       case 7: if (Cout % 256) return -4; rc = launch_wgrad2<DT, 4, 2, 1, 2, 2, 2>(a, s); break;
       case 9:
         if (Cout % 256) return -4;
-        if (W % 64 == 0 && Cin % 256 == 0 && mslice % 64 == 0 && (long long)a.M * Cout * 2 < 0x7fffffffLL &&
+        if ((W % 64 == 0 || rw) && Cin % 256 == 0 && gv.mslice % 64 == 0 && (long long)a.M * Cout * 2 < 0x7fffffffLL &&
             Cout <= 2048) {
           if (wsb_used) {
             Sb = kBiasParts;
             hipLaunchKernelGGL(bias_colsum_kernel<DT>, dim3(Sb), dim3(256), 0, s, a.dy, wsb_used, a.M, Cout, Sb);
           }
-          WgradArgs2 g = a;
+          WgradArgs2 g = gv;
           g.wsb = nullptr;
-          rc = launch_wgrad3<DT, 4, 2, 2>(g, s);
+          rc = rw ? launch_wgrad3<DT, 4, 2, 2, true>(g, s) : launch_wgrad3<DT, 4, 2, 2>(g, s);
         } else
           rc = launch_wgrad2<DT, 4, 2, 1, 2, 2, 2>(a, s);   // same tiles / slicing as cfg 7
         break;
@@ -1412,15 +1441,16 @@ static int conv_wgrad_impl(const void* dy, const void* x, float* ws, float* wsb,
       case 11: { // 128co x 256k v2 (Cout = 128); fallback = cfg 6 tiles
         const int tk = (cfg == 10) ? 128 : 256;
         if (Cout % (cfg == 10 ? 256 : 128)) return -4;
-        if (W % 64 == 0 && Cin % tk == 0 && K % tk == 0 && mslice % 64 == 0 &&
+        if ((W % 64 == 0 || rw) && Cin % tk == 0 && K % tk == 0 && gv.mslice % 64 == 0 &&
             (long long)a.M * Cout * 2 < 0x7fffffffLL && Cout <= 2048) {
           if (wsb_used) {
             Sb = kBiasParts;
             hipLaunchKernelGGL(bias_colsum_kernel<DT>, dim3(Sb), dim3(256), 0, s, a.dy, wsb_used, a.M, Cout, Sb);
           }
-          WgradArgs2 g = a;
+          WgradArgs2 g = gv;
           g.wsb = nullptr;
-          rc = (cfg == 10) ? launch_wgrad3<DT, 4, 2, 1>(g, s) : launch_wgrad3<DT, 2, 4, 1>(g, s);
+          if (rw) rc = (cfg == 10) ? launch_wgrad3<DT, 4, 2, 1, true>(g, s) : launch_wgrad3<DT, 2, 4, 1, true>(g, s);
+          else rc = (cfg == 10) ? launch_wgrad3<DT, 4, 2, 1>(g, s) : launch_wgrad3<DT, 2, 4, 1>(g, s);
         } else {
           rc = (cfg == 10) ? launch_wgrad2<DT, 4, 2, 1, 3, 1, 2>(a, s) : launch_wgrad2<DT, 2, 2, 1, 3, 2, 2>(a, s);
         }
@@ -1473,6 +1503,7 @@ static int conv_wgrad_1x1_batched_impl(const void* dy, const void* x, float* ws,
   a.H = M / W; a.W = W; a.Cin = Cin; a.Cout = Cout; a.ksize = 1; a.dil = 1; a.M = M; a.K = Cin;
   a.S = S; a.mslice = mslice;
   a.fdW = make_fastdiv((uint32_t)W); a.fdH = make_fastdiv((uint32_t)(M / W)); a.fdC = make_fastdiv((uint32_t)Cin);
+  a.Mreal = M; a.tx64 = W / 64; a.fdTX = make_fastdiv((uint32_t)a.tx64);
   a.nb = nb; a.dy_bs = dy_bs; a.x_bs = x_bs;
   int rc = launch_wgrad3<DT, 4, 2, 2>(a, s);
   if (rc) return rc;

@@ -72,12 +72,16 @@ def train_one_epoch_native(stepper, train_loader, device, epoch, log=None, log_e
     n = 0
     t0 = time.perf_counter()
     imgs = 0
+    pix = 0
     for step, batch in enumerate(loader):
         img, gt = prep(batch) if prep is not None else batch
         loss = stepper.step(img, gt)          # SUM of the per-rank losses (averaged below)
         total += loss.reshape(1) / max(1, get_world_size())
         n += 1
         imgs += img.shape[0] * get_world_size()
+        # NHWC4 (GPU-preprocessed) or NCHW input: per-pixel throughput for variable-size images
+        hw = img.shape[1] * img.shape[2] if (img.dim() == 4 and img.shape[-1] == 4) else img.shape[-2] * img.shape[-1]
+        pix += img.shape[0] * hw * get_world_size()
         if (step + 1) % log_every == 0:
             if stepper.nonfinite():
                 print("WARNING: non-finite loss, ending training")
@@ -91,6 +95,9 @@ def train_one_epoch_native(stepper, train_loader, device, epoch, log=None, log_e
                     log.log(kind="train", epoch=epoch, step=step + 1, mean_loss=ml, imgs_per_s=imgs / max(dt, 1e-9))
     if torch.device(device).type == "cuda":
         torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t0
+    stepper.last_epoch_stats = {"imgs": imgs, "mpix": pix / 1e6, "seconds": dt,
+                                "imgs_per_s": imgs / max(dt, 1e-9), "mpix_per_s": pix / 1e6 / max(dt, 1e-9)}
     if stepper.nonfinite():
         print("WARNING: non-finite loss, ending training")
         sys.exit(1)

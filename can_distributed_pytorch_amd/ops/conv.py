@@ -61,6 +61,22 @@ def to_nhwc4(img: torch.Tensor, dtype: torch.dtype = BF16) -> torch.Tensor:
     return out
 
 
+# Largest element count one conv launch addresses in any operand: the kernels index pixels x channels with 32-bit
+# offsets and read activations through 32-bit buffer resources (the v2 weight gradient needs M * Cout * 2 < 2^31).
+# A batch beyond it runs as consecutive launches over image chunks (images are independent in every conv; weight
+# gradients accumulate over the chunks with beta = 1), so batch size is bounded by HBM, not by the index width.
+MAX_ELEMS_PER_LAUNCH = 1 << 30
+
+
+def image_chunks(n: int, elems_per_image: int, limit: Optional[int] = None):
+    """[(i0, i1)] image ranges whose operands stay within ``limit`` (default MAX_ELEMS_PER_LAUNCH) elements."""
+    limit = limit or MAX_ELEMS_PER_LAUNCH
+    if elems_per_image > limit:
+        raise ValueError(f"one image needs {elems_per_image} elements per operand (> {limit}): too large for one launch")
+    per = max(1, limit // elems_per_image)
+    return [(i, min(n, i + per)) for i in range(0, n, per)]
+
+
 def _check_act(x: torch.Tensor, name: str, c: Optional[int] = None, dtype: Optional[torch.dtype] = None):
     if not x.is_cuda:
         raise ValueError(f"{name} must be a GPU tensor")
@@ -124,8 +140,6 @@ def conv_igemm(x: torch.Tensor, wpack: torch.Tensor, bias: Optional[torch.Tensor
         if tuple(out.shape) != oshape:
             raise ValueError("out has the wrong shape")
         _check_act(out, "out", dtype=dt)
-    if n * h * w >= 2 ** 31 // max(ci, co):
-        raise ValueError("tensor too large for 32-bit pixel indexing")
     bp_ptr, bp_cap = 0, 0
     if bias_part is not None:
         if epi not in (EPI_MASK, EPI_POOLBWD):
@@ -134,6 +148,23 @@ def conv_igemm(x: torch.Tensor, wpack: torch.Tensor, bias: Optional[torch.Tensor
                 bias_part.shape[1] != co:
             raise ValueError(f"bias_part must be a contiguous fp32 [rows, {co}] tensor")
         bp_ptr, bp_cap = bias_part.data_ptr(), bias_part.shape[0]
+    chunks = image_chunks(n, h * w * max(ci, co) * (4 if epi == EPI_POOLBWD else 1))
+    if len(chunks) > 1:
+        # consecutive launches over image chunks; bias partial rows are written back to back
+        r0, none_rows = 0, False
+        for i0, i1 in chunks:
+            res = conv_igemm(x[i0:i1], wpack, bias, ksize=ksize, dil=dil, epi=epi,
+                             mask=mask[i0:i1] if mask is not None else None, out=out[i0:i1], first=first, tile=tile,
+                             bias_part=bias_part[r0:] if bias_part is not None else None)
+            if bias_part is not None:
+                part = res[1]
+                if part is None:
+                    none_rows = True
+                else:
+                    r0 += part.shape[0]
+        if bias_part is not None:
+            return out, (None if none_rows or r0 == 0 else bias_part[:r0])
+        return out
     rows = C.conv_igemm(x.data_ptr(), wpack.data_ptr(), bias.data_ptr() if bias is not None else 0,
                         mask.data_ptr() if mask is not None else 0, out.data_ptr(), n, h, w, ci, co, ksize, dil,
                         epi, int(first), tile, dt_code(dt), _ext.stream_ptr(x.device), bp_ptr, bp_cap)
@@ -179,8 +210,11 @@ BIAS_ROWS = 512     # bias partial rows the weight-gradient reduce kernels take 
 def bias_part_capacity(n: int, h: int, w: int) -> int:
     """Rows a data-gradient epilogue may write for an output of n x h x w pixels (pooled resolution for
     EPI_POOLBWD): LDS-DMA kernels one row per (pixel tile, wave slot) = ceil(M / 64) at most, the halo
-    kernel one per (4 x 64 tile, wave slot)."""
-    return max(-(-n * h * w // 64) + 64, n * (-(-h // 4)) * (-(-w // 64)) * 8)
+    kernel one per (4 x 64 tile, wave slot), the row ring one per (per-image 2- or 4-row x 128-column tile, wave
+    slot) (ragged tiles included)."""
+    cb = -(-w // 128)
+    return max(-(-n * h * w // 64) + 64, n * (-(-h // 4)) * (-(-w // 64)) * 8,
+               n * (-(-h // 2)) * cb * 4, n * (-(-h // 4)) * cb * 8)
 
 
 def conv_dgrad_with_bias(dy: torch.Tensor, wpack: torch.Tensor, *, ksize: int, dil: int = 1, epi: int = EPI_MASK,
@@ -286,6 +320,16 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, db: Optional
     if db is not None and (db.dtype != torch.float32 or db.numel() != co or not db.is_contiguous()):
         raise ValueError("db must be contiguous fp32 [Co]")
     ws = ws or WgradWorkspace(x.device)
+    chunks = image_chunks(n, h * w * max(ci, co))
+    if len(chunks) > 1:
+        # dW (and db) accumulate over image chunks: the first launch applies beta, the others add (beta = 1); bias
+        # partials of the whole dY (one list) are reduced by the first launch only
+        for c, (i0, i1) in enumerate(chunks):
+            use_bp = bias_partials is not None and db is not None
+            conv_wgrad(dy[i0:i1], x[i0:i1], dw, db if (c == 0 or not use_bp) else None, ksize=ksize, dil=dil,
+                       first=first, ws=ws, beta=beta if c == 0 else 1.0, scale=scale, dscale=dscale,
+                       bias_partials=bias_partials if c == 0 else None)
+        return
     s, mslice, cfg, need = ws.plan(n * h * w, ci, co, ksize, first, dil)
     buf = ws.reserve(need)
     ktot = 64 if first else ksize * ksize * ci
@@ -332,6 +376,8 @@ def wgrad_1x1_batched_ok(dy: torch.Tensor, x: torch.Tensor, dws) -> bool:
     ci = x.shape[-1]
     if tuple(x.shape[:4]) != (nb, n, h, w) or w % 64 or co % 256 or ci % 256 or (n * h * w) % 64:
         return False
+    if n * h * w * max(ci, co) * 2 >= 2 ** 31:
+        return False                       # 32-bit operand addressing: the per-item launches chunk instead
     if len(dws) != nb or any(d.dtype != torch.float32 or not d.is_contiguous() or tuple(d.shape) != (co, ci, 1, 1)
                              for d in dws):
         return False
@@ -388,8 +434,6 @@ def conv_pool_fwd(x: torch.Tensor, wpack: torch.Tensor, bias: torch.Tensor, *, k
         raise ValueError("bias must be contiguous fp32 [Cout]")
     if not conv_pool_fwd_ok(x, co, ksize, tile):
         raise ValueError(f"fused pool needs H even and W a multiple of the tile half-width ({list(x.shape)})")
-    if n * h * w >= 2 ** 31 // max(ci, co):
-        raise ValueError("tensor too large for 32-bit pixel indexing")
     if not keep_full and out is not None:
         raise ValueError("out given with keep_full=False")
     for t, shp, name in ((out, (n, h, w, co), "out"), (pooled, (n, h // 2, w // 2, co), "pooled")):
@@ -402,6 +446,15 @@ def conv_pool_fwd(x: torch.Tensor, wpack: torch.Tensor, bias: torch.Tensor, *, k
     if pooled is None:
         pooled = torch.empty(n, h // 2, w // 2, co, dtype=dt, device=x.device)
     cd = torch.empty(n, h // 2, w // 2, co // 8, dtype=torch.int32, device=x.device) if codes else None
+    chunks = image_chunks(n, h * w * max(ci, co))
+    if len(chunks) > 1:
+        for i0, i1 in chunks:
+            xs = x[i0:i1]
+            C.conv_pool_fwd(xs.data_ptr(), wpack.data_ptr(), bias.data_ptr(),
+                            out[i0:i1].data_ptr() if out is not None else 0, pooled[i0:i1].data_ptr(),
+                            cd[i0:i1].data_ptr() if cd is not None else 0, i1 - i0, h, w, ci, co, ksize, dil, tile,
+                            dt_code(dt), _ext.stream_ptr(x.device))
+        return out, pooled, cd
     C.conv_pool_fwd(x.data_ptr(), wpack.data_ptr(), bias.data_ptr(), out.data_ptr() if out is not None else 0,
                     pooled.data_ptr(), cd.data_ptr() if cd is not None else 0, n, h, w, ci, co, ksize, dil, tile,
                     dt_code(dt), _ext.stream_ptr(x.device))
@@ -443,6 +496,14 @@ def conv_dgrad_w1g(dy: torch.Tensor, wpack: torch.Tensor, mask: torch.Tensor, im
     if slabs.dim() != 2 or slabs.shape[1] != 36 * 64 or tuple(bslabs.shape) != (cap, 64):
         raise ValueError("slabs / bslabs must be [cap, 36*64] / [cap, 64]")
     out = torch.empty_like(dy) if store_dx else None
+    chunks = image_chunks(n, h * w * 64)
+    if len(chunks) > 1:
+        for c, (i0, i1) in enumerate(chunks):
+            o = conv_dgrad_w1g(dy[i0:i1], wpack, mask[i0:i1], img[i0:i1], dw1, db1, slabs=slabs, bslabs=bslabs,
+                               store_dx=store_dx, beta=beta if c == 0 else 1.0, scale=scale, dscale=dscale)
+            if out is not None:
+                out[i0:i1].copy_(o)
+        return out
     st = _ext.stream_ptr(dy.device)
     s = C.conv_ws64_dgrad_w1g(dy.data_ptr(), wpack.data_ptr(), mask.data_ptr(), img.data_ptr(),
                               out.data_ptr() if out is not None else 0, slabs.data_ptr(), bslabs.data_ptr(), cap,
@@ -479,8 +540,10 @@ def conv_ctx_fwd(fv: torch.Tensor, wcat: torch.Tensor, t: torch.Tensor, u: torch
     _check_cells(u, n, c, "u")
     wts = torch.empty(n, h, w, 4 * c, dtype=fv.dtype, device=fv.device)
     cat = torch.empty(n, h, w, 2 * c, dtype=fv.dtype, device=fv.device)
-    C.conv_ctx(1, fv.data_ptr(), wcat.data_ptr(), t.data_ptr(), u.data_ptr(), fv.data_ptr(), cat.data_ptr(),
-               wts.data_ptr(), n, h, w, c, dt_code(fv.dtype), _ext.stream_ptr(fv.device))
+    for i0, i1 in image_chunks(n, h * w * 4 * c):
+        C.conv_ctx(1, fv[i0:i1].data_ptr(), wcat.data_ptr(), t[i0:i1].data_ptr(), u[i0:i1].data_ptr(),
+                   fv[i0:i1].data_ptr(), cat[i0:i1].data_ptr(), wts[i0:i1].data_ptr(), i1 - i0, h, w, c,
+                   dt_code(fv.dtype), _ext.stream_ptr(fv.device))
     return wts, cat
 
 
@@ -517,6 +580,8 @@ def conv_ctx_bwd(dg: torch.Tensor, wcat_dgr: torch.Tensor, dave: torch.Tensor, d
         raise ValueError(f"wcat_dgr must be a contiguous {fv.dtype} [{c}, {4 * c}] pack")
     _check_cells(dave, n, c, "dave")
     dfv = torch.empty_like(fv)
-    C.conv_ctx(0, dg.data_ptr(), wcat_dgr.data_ptr(), dave.data_ptr(), 0, fv.data_ptr(), dcat.data_ptr(),
-               dfv.data_ptr(), n, h, w, c, dt_code(fv.dtype), _ext.stream_ptr(fv.device))
+    for i0, i1 in image_chunks(n, h * w * 4 * c):
+        C.conv_ctx(0, dg[i0:i1].data_ptr(), wcat_dgr.data_ptr(), dave[i0:i1].data_ptr(), 0, fv[i0:i1].data_ptr(),
+                   dcat[i0:i1].data_ptr(), dfv[i0:i1].data_ptr(), i1 - i0, h, w, c, dt_code(fv.dtype),
+                   _ext.stream_ptr(fv.device))
     return dfv

@@ -20,6 +20,13 @@ from can_distributed_pytorch_amd.data.synthetic import (IMAGENET_MEAN, IMAGENET_
                                                         density_from_points_fixed, synthetic_points)
 
 
+# ShanghaiTech Part A mixes image sizes (mostly <= 1024 on the long side, landscape and portrait); these (H, W) pairs
+# follow that spread.  After CrowdDataset's resize to multiples of 8 most widths are not multiples of 128, so the
+# native kernels run their ragged (masked) tiles.
+MIXED_SIZES = [(768, 1024), (683, 1024), (1024, 768), (576, 768), (480, 640), (400, 600), (600, 800), (765, 1020),
+               (532, 800), (704, 1000), (450, 680), (1000, 667), (620, 900), (384, 512), (720, 960), (510, 760)]
+
+
 def render(seed, h, w, heads=(100, 1500)):
     gen = torch.Generator().manual_seed(seed)
     n = int(torch.randint(heads[0], heads[1] + 1, (1,), generator=gen))
@@ -49,6 +56,9 @@ def main():
     ap.add_argument("--height", type=int, default=768)
     ap.add_argument("--width", type=int, default=1024)
     ap.add_argument("--workers", type=int, default=8)
+    ap.add_argument("--mixed", action="store_true",
+                    help="ShanghaiTech-A-like mixed sizes (landscape / portrait, W %% 128 != 0 for most) instead of "
+                         "--height x --width")
     a = ap.parse_args()
     _ = (IMAGENET_MEAN, IMAGENET_STD)
     from multiprocessing import Pool
@@ -56,7 +66,10 @@ def main():
         idir, gdir = os.path.join(a.root, part, "images"), os.path.join(a.root, part, "ground_truth")
         os.makedirs(idir, exist_ok=True)
         os.makedirs(gdir, exist_ok=True)
-        jobs = [(idir, gdir, k, off + k, a.height, a.width) for k in range(n)]
+        if a.mixed:
+            jobs = [(idir, gdir, k, off + k) + MIXED_SIZES[(off + k) % len(MIXED_SIZES)] for k in range(n)]
+        else:
+            jobs = [(idir, gdir, k, off + k, a.height, a.width) for k in range(n)]
         with Pool(a.workers) as pool:
             for i, _k in enumerate(pool.imap_unordered(_write, jobs)):
                 if (i + 1) % 64 == 0:

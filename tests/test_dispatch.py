@@ -87,3 +87,12 @@ def test_binary_tied_to_sources(monkeypatch):
     monkeypatch.setattr(build_native, "source_hash", lambda files=None: "0" * 64)
     with pytest.raises(RuntimeError, match="stale native extension"):
         _ext.check_source_hash(m)
+
+
+def test_in_tree_binary_imports():
+    """A built _C must import (an undefined symbol only shows up at import time, e.g. on the GPU box)."""
+    from can_distributed_pytorch_amd import build_native
+    from can_distributed_pytorch_amd.ops import _ext
+    if not os.path.exists(build_native.ext_path()):
+        pytest.skip("native extension not built")
+    assert _ext.load() is not None, f"in-tree _C does not import: {_ext._err}"

@@ -29,7 +29,9 @@ def _ref_context(model, fv):
     return torch.cat((fv, num / (den + 1e-12)), 1)
 
 
-def _run(dispatch_cfg, linear, n, h, w, seed):
+def _run(dispatch_cfg, linear, n, h, w, seed, dtype=torch.bfloat16, beta=0.0, dscale=None):
+    """beta: accumulate into pre-filled gradient buffers; dscale: the fp16 step's 1 / loss scale (dcat carries the
+    scale 1 / dscale, the weight gradients must come out unscaled, d(fv) keeps the scale)."""
     from can_distributed_pytorch_amd.models import CANNet
     from can_distributed_pytorch_amd.ops.executor import CANNetExecutor
     from can_distributed_pytorch_amd.ops import conv as C
@@ -40,10 +42,10 @@ def _run(dispatch_cfg, linear, n, h, w, seed):
         for s in SCALES:
             getattr(model, f"conv{s}_1").weight.normal_(0, 0.05)
             getattr(model, f"conv{s}_2").weight.normal_(0, 0.05)
-    ex = CANNetExecutor(model)
+    ex = CANNetExecutor(model, dtype=dtype)
     ex.refresh_packs(force=True)
     c = 512
-    fv = (torch.randn(n, h, w, c, device="cuda") + 0.3).to(torch.bfloat16)
+    fv = (torch.randn(n, h, w, c, device="cuda") + 0.3).to(dtype)
     if linear:
         assert C.ctx_linear_ok(fv)
     cat, saved = ex._context_fwd(fv, save=True)
@@ -53,12 +55,20 @@ def _run(dispatch_cfg, linear, n, h, w, seed):
     cr = _ref_context(model, fr)
     e_fwd = _rel(cat.float().permute(0, 3, 1, 2), cr)
     # backward from a random dcat (16-bit, as the B1 data gradient delivers it)
-    dcat = torch.randn(n, h, w, 2 * c, device="cuda").to(torch.bfloat16)
+    dcat = torch.randn(n, h, w, 2 * c, device="cuda").to(dtype)
     params = list(model.parameters())
-    grads = [torch.zeros_like(p) for p in params]
+    grads0 = [torch.randn_like(p) if beta else torch.zeros_like(p) for p in params]
+    grads = [g.clone() for g in grads0]
     ws = C.WgradWorkspace(fv.device)
-    dpre = ex._context_bwd(saved, fv, dcat, grads, ws, 0.0, 1.0, lambda idx: None)
+    lscale = 1.0
+    dsc = None
+    if dscale is not None:
+        lscale = 1.0 / dscale
+        dsc = torch.tensor([dscale], dtype=torch.float32, device="cuda")
+    dcat_in = (dcat.float() * lscale).to(dtype)              # exact: a power-of-two scale
+    dpre = ex._context_bwd(saved, fv, dcat_in, grads, ws, beta, 1.0, lambda idx: None, dsc)
     torch.cuda.synchronize()
+    dpre = dpre.float() / lscale
     refs = torch.autograd.grad(cr, [fr] + [getattr(model, f"conv{s}_{k}").weight for s in SCALES for k in (1, 2)],
                                dcat.float().permute(0, 3, 1, 2))
     dfv_ref = refs[0] * (fr > 0)
@@ -69,7 +79,7 @@ def _run(dispatch_cfg, linear, n, h, w, seed):
         for k in (1, 2):
             p = getattr(model, f"conv{s}_{k}").weight
             idx = next(j for j, q in enumerate(params) if q is p)
-            e_w[f"conv{s}_{k}"] = _rel(grads[idx], refs[i])
+            e_w[f"conv{s}_{k}"] = _rel(grads[idx] - beta * grads0[idx], refs[i])
             i += 1
     return e_fwd, e_dfv, e_w
 
@@ -79,6 +89,17 @@ def _run(dispatch_cfg, linear, n, h, w, seed):
 def test_context_linear_vs_fp32(dispatch_cfg, n, h, w, tile):
     dispatch_cfg(ctx_tile_f=int(tile), ctx_tile_b=int(tile))
     e_fwd, e_dfv, e_w = _run(dispatch_cfg, True, n, h, w, seed=n * 100 + h)
+    assert e_fwd < 5e-3, e_fwd
+    assert e_dfv < 2e-2, e_dfv
+    assert all(v < 2e-2 for v in e_w.values()), e_w
+
+
+@pytest.mark.parametrize("dtype,beta,dscale", [(torch.bfloat16, 1.0, None), (torch.float16, 0.0, 0.25),
+                                               (torch.float16, 1.0, 0.5)])
+def test_context_linear_accumulate_and_loss_scale(dispatch_cfg, dtype, beta, dscale):
+    """The linearised backward's beta != 0 path (ctx_w2_scatter + ctx_gemm mode 2 accumulating into pre-filled
+    gradients), the fp16 loss-scale path (dscale folded into every context weight gradient) and fp16 dG storage."""
+    e_fwd, e_dfv, e_w = _run(dispatch_cfg, True, 2, 12, 96, seed=41, dtype=dtype, beta=beta, dscale=dscale)
     assert e_fwd < 5e-3, e_fwd
     assert e_dfv < 2e-2, e_dfv
     assert all(v < 2e-2 for v in e_w.values()), e_w

@@ -235,8 +235,10 @@ def main(args):
             ips = len(train_loader) * args.batch_size * world / max(t_train, 1e-9)
             print(f"[epoch {epoch}] loss: {mean_loss:.4f} mae: {mean_mae:.3f}, min_mae: {min_mae:.3f}, "
                   f"min_epoch: {min_epoch}, train img/s {ips:.1f}")
+            st = getattr(stepper, "last_epoch_stats", None) or {}
             log.log(kind="epoch", epoch=epoch, loss=mean_loss, mae=mean_mae, min_mae=min_mae, lr=lr_now,
-                    train_imgs_per_s=ips, train_s=t_train)
+                    train_imgs_per_s=ips, train_s=t_train, train_mpix_per_s=st.get("mpix_per_s"),
+                    train_loop_imgs_per_s=st.get("imgs_per_s"), batch_size=args.batch_size, world=world)
             if use_wandb:
                 wandb_log(loss=mean_loss, mae=mean_mae, lr=lr_now)
         barrier()
