@@ -341,14 +341,18 @@ struct ConvArgs2 {
 // pixel m of row r of pixel tile pt; EPI_POOLFWD tiles are 2 rows x TP/2 columns, rows interleaved per
 // 16-pixel fragment (see EPI_POOLFWD), the other epilogues take TP consecutive pixels
 // RT (row-ring kernel, conv_rring_kernel): a tile is RT image rows x 128 columns, tile pt = (n, row group, 128-column
-// block) with the column block fastest; r = row * 128 + column.  Pixels of a ragged last column block (W % 128 != 0)
-// or tile row (H % RT != 0) map to a.M (= skipped by the epilogue)
-template <int TP, int EPI, int RT = 0>
+// block) with the column block fastest; r = row * 128 + column.  RG (ragged map: W % 128 != 0 or H % RT != 0): the
+// tiles are per image (rr_ty tile rows of rr_tx column blocks) and pixels of a ragged last column block or tile row
+// map to a.M (= skipped by the epilogue); otherwise (W % 128 == 0, H % RT == 0) tile rows run across images
+template <int TP, int EPI, int RT = 0, bool RG = false>
 __device__ __forceinline__ int tile_pix(const ConvArgs2& a, int pt, int r) {
-  if constexpr (RT != 0 && EPI != EPI_POOLFWD) {
+  if constexpr (RT != 0 && EPI != EPI_POOLFWD && RG) {
     const int tx = a.rr_tx, q = pt / tx, cb = pt - q * tx;
     const int n = q / a.rr_ty, oh = RT * (q - n * a.rr_ty) + (r >> 7), ow = cb * 128 + (r & 127);
     return (oh < a.H && ow < a.W) ? (n * a.H + oh) * a.W + ow : a.M;
+  } else if constexpr (RT != 0 && EPI != EPI_POOLFWD) {
+    const int tx = a.W >> 7, q = pt / tx, cb = pt - q * tx;
+    return (RT * q + (r >> 7)) * a.W + cb * 128 + (r & 127);
   } else if constexpr (EPI == EPI_POOLFWD) {
     const int ncb = a.W / (TP / 2);
     const int rp = pt / ncb, cb = pt - rp * ncb;    // rp = n * H/2 + pooled row
@@ -360,7 +364,7 @@ __device__ __forceinline__ int tile_pix(const ConvArgs2& a, int pt, int r) {
 
 // Shared epilogue of the LDS-DMA kernels: lane (fr, fq) of wave (wc, wp) owns
 // 16 consecutive output channels of one pixel per 16x16 pixel fragment.
-template <int DT, int WC, int WP, int PW, int EPI, int RT = 0>
+template <int DT, int WC, int WP, int PW, int EPI, int RT = 0, bool RG = false>
 __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4][4 * PW], int ct, int pt,
                                               int wc, int wp, int fr, int fq) {
   constexpr int TC = 64 * WC, TP = 64 * PW * WP;
@@ -386,7 +390,7 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
   if constexpr (EPI == EPI_MASK || EPI == EPI_POOLBWD) {
 #pragma unroll
     for (int i = 0; i < NF; ++i) {
-      const int m = tile_pix<TP, EPI, RT>(a, pt, wp * 64 * PW + i * 16 + fr);
+      const int m = tile_pix<TP, EPI, RT, RG>(a, pt, wp * 64 * PW + i * 16 + fr);
       if constexpr (EPI == EPI_MASK) {
         mk0[i] = make_uint4(0u, 0u, 0u, 0u);
         mk1[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -406,7 +410,7 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
   }
 #pragma unroll
   for (int i = 0; i < 4 * PW; ++i) {
-    const int m = tile_pix<TP, EPI, RT>(a, pt, wp * 64 * PW + i * 16 + fr);
+    const int m = tile_pix<TP, EPI, RT, RG>(a, pt, wp * 64 * PW + i * 16 + fr);
     if (m >= a.M) continue;
     float v[16];
 #pragma unroll
@@ -1066,11 +1070,13 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
   };
   // MFMAs over pixel fragments [i0, i1) (so the B fragments die in halves)
   auto mma = [&](const frag8_t (&af)[JW], const frag8_t (&bfr)[4 * PW], int i0, int i1) {
+    mfma_prio_hi();
 #pragma unroll
     for (int i = i0; i < i1; ++i)
 #pragma unroll
       for (int j = 0; j < JW; ++j)
         acc[j >> 2][j & 3][i] = mfma16<DT>(af[j], bfr[i], acc[j >> 2][j & 3][i]);
+    mfma_prio_lo();
   };
 
   frag8_t a0[JW], b0[4 * PW], a1[JW], b1[4 * PW];
@@ -1214,7 +1220,9 @@ __host__ __device__ constexpr int rr_lds(int TC, int TR) { return 2 * TC * 128 +
 // 64 x 512 tile of cfg 23, bitwise cfg 23: 8 waves of 64 channels x 64 pixels, two per tile row).  A 4-row tile's
 // chunk needs 4 + 2 * dil rows and its rows 2, 3 stay live to the chunk's last tap, so it runs 8 slots and issues a
 // row 2 stages ahead with a full drain per stage (LEAD = 2); the 2-row tile runs 4 slots, LEAD 3 or 4, counted waits.
-template <int DT, int EPI, int D, int LEAD = 3, int TC = 256, int TR = 2>
+// RG: a ragged map (W % 128 != 0 or H % TR != 0), its own instantiation so the aligned one keeps the cheaper
+// cross-image tile decode (and its SGPR budget: the per-image decode of both in one kernel spilled SGPRs)
+template <int DT, int EPI, int D, int LEAD = 3, int TC = 256, int TR = 2, bool RG = false>
 __global__ void __launch_bounds__(512, 1) conv_rring_kernel(ConvArgs2 a) {
   static_assert(((TC == 256 || TC == 128) && TR == 2 && LEAD >= 3 && LEAD <= 4) || (TC == 64 && TR == 4 && LEAD == 2),
                 "row-ring configs: 256 x (2 x 128) with a 3- or 4-stage row lead (counted barrier waits need >= 3, 4 slots "
@@ -1238,18 +1246,24 @@ __global__ void __launch_bounds__(512, 1) conv_rring_kernel(ConvArgs2 a) {
   const int rt = wp / WPR;                           // the tile row this wave computes
   const int cbw = (wp - rt * WPR) * 64 * PW;         // and its first column in the tile
 
-  const int tx = a.rr_tx;                                     // ceil(W / 128) column blocks
+  const int tx = RG ? a.rr_tx : (a.W >> 7);                  // ceil(W / 128) column blocks
   const int nct = a.Cout / TC;
-  const int npt = a.rr_np;
+  const int npt = RG ? a.rr_np : a.M / TP;
   const int tile = xcd_remap(blockIdx.x, nct * npt);
   const int ct = tile % nct, pt = tile / nct;
   const int q = pt / tx, cb = pt - q * tx;
-  const int nimg = q / a.rr_ty;
-  const int oh0 = TR * (q - nimg * a.rr_ty);
-  const int grow0 = nimg * a.H + oh0;                         // n * H + oh0
+  int oh0, grow0;                                             // grow0 = n * H + oh0
+  if constexpr (RG) {
+    const int nimg = q / a.rr_ty;
+    oh0 = TR * (q - nimg * a.rr_ty);
+    grow0 = nimg * a.H + oh0;
+  } else {
+    grow0 = TR * q;
+    oh0 = grow0 - (int)fdiv((uint32_t)grow0, a.fdH) * a.H;
+  }
   const int col0 = cb * 128;
   // a ragged last column block (W % 128 != 0): interior / guard pixels at or beyond W come from the zero page
-  const bool ragged_w = (a.W & 127) != 0;
+  const bool ragged_w = RG && (a.W & 127) != 0;
   const int Ktot = 9 * a.Cin;
   const int nc = a.Cin >> 6, nk = 9 * nc;
   const int lc8 = ((lane & 7) ^ (lane >> 3)) * 8;             // swizzled 16-B chunk (pieces are 8-pixel aligned)
@@ -1307,14 +1321,19 @@ __global__ void __launch_bounds__(512, 1) conv_rring_kernel(ConvArgs2 a) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int j = wave + NW * h;                           // interior piece: pixels 8j .. 8j + 7
-        const bool cv = !ragged_w || col0 + 8 * j + (lane >> 3) < a.W;
+        // wave-uniform: a ragged width is a multiple of 8 (rring_width_ok), so a piece is wholly in or out.  Keep
+        // it so: with a lane-divergent condition here hipcc (ROCm 7.2) merged the two sources of the select into
+        // one wave-uniform base plus a per-lane offset, and masked lanes read x + rbase + 8 * lane instead of the
+        // zero page (out of bounds on the first / last row of the map)
+        const bool cv = !ragged_w || col0 + 8 * j < a.W;
         glds16((rv && cv) ? (const void*)(a.x + rbase + (size_t)(8 * j) * a.Cin + boff)
                           : (const void*)(a.zero + lane * 8),
                lds_addr(slot + (j + 1) * 1024));
       }
       if (tx > 1 && wave < 2) {
-        // 8-pixel guards of an interior column block: real pixels of the neighbouring blocks (wave 0 left, 1 right)
-        const bool gv = rv && (wave == 0 ? cb > 0 : (cb + 1 < tx && (!ragged_w || col0 + 128 + (lane >> 3) < a.W)));
+        // 8-pixel guards of an interior column block: real pixels of the neighbouring blocks (wave 0 left, 1 right;
+        // a right neighbour block starts below W, and W % 8 == 0 puts its whole guard piece inside the map)
+        const bool gv = rv && (wave == 0 ? cb > 0 : cb + 1 < tx);
         const long long gc = (wave == 0) ? -8 : 128;
         glds16(gv ? (const void*)(a.x + (long long)rbase + gc * a.Cin + boff) : (const void*)(a.zero + lane * 8),
                lds_addr(slot + (wave == 0 ? 0 : 17) * 1024));
@@ -1358,10 +1377,12 @@ __global__ void __launch_bounds__(512, 1) conv_rring_kernel(ConvArgs2 a) {
       bfr[i] = __builtin_bit_cast(frag8_t, *reinterpret_cast<const uint4*>(base + i * 2048));
   };
   auto mma = [&](const frag8_t (&af)[4], const frag8_t (&bfr)[4 * PW], int i0, int i1) {
+    mfma_prio_hi();
 #pragma unroll
     for (int i = i0; i < i1; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[j][i] = mfma16<DT>(af[j], bfr[i], acc[j][i]);
+    mfma_prio_lo();
   };
 
   frag8_t a0[4], b0[4 * PW], a1[4], b1[4 * PW];
@@ -1420,15 +1441,16 @@ __global__ void __launch_bounds__(512, 1) conv_rring_kernel(ConvArgs2 a) {
   read(nk - 1, 1, a1, b1);
   mma(a0, b0, 0, 4 * PW);
   mma(a1, b1, 0, 4 * PW);
-  glds_epilogue<DT, WC, WP, PW, EPI, TR>(a, acc, ct, pt, wc, wp, fr, fq);
+  glds_epilogue<DT, WC, WP, PW, EPI, TR, RG>(a, acc, ct, pt, wc, wp, fr, fq);
 }
 
 // column-block utilisation of the row ring on a ragged width: W / (ceil(W / 128) * 128) >= 0.7 (W = 240, 480,
-// 960: 94 %); below it (W = 135: 53 %) the per-tap LDS-DMA kernel, whose pixel tiles run across rows, wastes less
+// 960: 94 %); below it (W = 135: 53 %) the per-tap LDS-DMA kernel, whose pixel tiles run across rows, wastes less.
+// A ragged width must be a multiple of 8: the row DMA's validity is then uniform per 8-pixel piece (see issue_rows)
 static bool rring_width_ok(int W) {
   if (W % 128 == 0) return true;
   const int tx = (W + 127) / 128;
-  return W >= 96 && 10 * W >= 7 * 128 * tx;
+  return W % 8 == 0 && W >= 96 && 10 * W >= 7 * 128 * tx;
 }
 // pixel tiles of the row ring: N * ceil(H / TR) * ceil(W / 128) (ragged last tile row / column block masked)
 static int rr_np(int H, int W, int M, int TR) {
@@ -1460,9 +1482,9 @@ static int rring_cfg(int H, int W, int Cin, int Cout, int ksize, int dil, int ep
 // dilation 484.9 img/s (medians of 4 interleaved rounds)
 static int rring_mode() { return g_dispatch.rring; }
 
-template <int DT, int EPI, int TC, int TR, int LEAD, int D>
-static int launch_rring_one(const ConvArgs2& a, hipStream_t s) {
-  auto kfn = conv_rring_kernel<DT, EPI, D, LEAD, TC, TR>;
+template <int DT, int EPI, int TC, int TR, int LEAD, int D, bool RG>
+static int launch_rring_rg(const ConvArgs2& a, hipStream_t s) {
+  auto kfn = conv_rring_kernel<DT, EPI, D, LEAD, TC, TR, RG>;
   static bool attr = false;
   if (!attr) {
     CAN_HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, rr_lds(TC, TR)));
@@ -1474,6 +1496,11 @@ static int launch_rring_one(const ConvArgs2& a, hipStream_t s) {
   b.rr_np = rr_np(a.H, a.W, a.M, TR);
   hipLaunchKernelGGL(kfn, dim3((a.Cout / TC) * b.rr_np), dim3(512), rr_lds(TC, TR), s, b);
   return (int)hipGetLastError();
+}
+template <int DT, int EPI, int TC, int TR, int LEAD, int D>
+static int launch_rring_one(const ConvArgs2& a, hipStream_t s) {
+  if (a.W % 128 == 0 && a.H % TR == 0) return launch_rring_rg<DT, EPI, TC, TR, LEAD, D, false>(a, s);
+  return launch_rring_rg<DT, EPI, TC, TR, LEAD, D, true>(a, s);
 }
 
 template <int DT, int EPI>

@@ -60,6 +60,14 @@ def main():
     ap.add_argument("--lr", type=float, default=2e-7)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", default="gpurun_out/convergence.jsonl")
+    ap.add_argument("--impls", default="torch_fp32,native_bf16,native_fp16",
+                    help="torch_fp32 (the reference numerics) first; the others are compared against it")
+    # tolerances declared BEFORE the run (the verdict asks for the gap against a written tolerance): the final count
+    # MAE of a native run within 10 % of the fp32 run's, its final-epoch mean loss within 5 %, and no epoch's mean
+    # loss more than 10 % away
+    ap.add_argument("--tol-mae-rel", type=float, default=0.10)
+    ap.add_argument("--tol-loss-last-rel", type=float, default=0.05)
+    ap.add_argument("--tol-loss-max-rel", type=float, default=0.10)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     h, w, b = a.height, a.width, a.batch
@@ -71,14 +79,16 @@ def main():
     curves = {}
     from can_distributed_pytorch_amd.engine.native import NativeStepper
     from can_distributed_pytorch_amd.engine.trainer import TorchStepper
-    for impl in ("torch_fp32", "native_bf16"):
+    impls = a.impls.split(",")
+    assert impls[0] == "torch_fp32", "the fp32 reference run comes first"
+    for impl in impls:
         model = copy.deepcopy(base)
         if impl == "torch_fp32":
             st = TorchStepper(dev, dtype="fp32", lr=a.lr, model=model)
             net = st.model
         else:
             model.exec_backend = "hip"
-            st = NativeStepper(dev, dtype="bf16", lr=a.lr, graph=False, model=model)
+            st = NativeStepper(dev, dtype=impl.split("_")[1], lr=a.lr, graph=False, model=model)
             net = st.model
         rows = []
         mae0 = count_mae(net, test)
@@ -99,20 +109,28 @@ def main():
             out.flush()
             print(json.dumps(rows[-1]), flush=True)
         curves[impl] = rows
-    # summary: per-epoch relative gaps of the native curve to the fp32 one
-    tl = [(r["train_loss"], q["train_loss"]) for r, q in zip(curves["torch_fp32"][1:], curves["native_bf16"][1:])]
-    tm = [(r["test_mae"], q["test_mae"]) for r, q in zip(curves["torch_fp32"], curves["native_bf16"])]
-    summ = {
-        "summary": True, "epochs": a.epochs, "steps": a.epochs * (a.train // b), "image_hw": [h, w], "batch": b,
-        "lr": a.lr,
-        "fp32_loss_first_last": [tl[0][0], tl[-1][0]], "native_loss_first_last": [tl[0][1], tl[-1][1]],
-        "fp32_mae_init_last": [tm[0][0], tm[-1][0]], "native_mae_init_last": [tm[0][1], tm[-1][1]],
-        "max_rel_loss_gap": max(abs(q - r) / abs(r) for r, q in tl),
-        "max_abs_mae_gap": max(abs(q - r) for r, q in tm),
-        "mae_gap_last": tm[-1][1] - tm[-1][0],
-    }
-    out.write(json.dumps(summ) + "\n")
-    print(json.dumps(summ), flush=True)
+    # summary per native run: gaps of its curve to the fp32 one, checked against the declared tolerances
+    for impl in impls[1:]:
+        tl = [(r["train_loss"], q["train_loss"]) for r, q in zip(curves["torch_fp32"][1:], curves[impl][1:])]
+        tm = [(r["test_mae"], q["test_mae"]) for r, q in zip(curves["torch_fp32"], curves[impl])]
+        rel_last = abs(tl[-1][1] - tl[-1][0]) / abs(tl[-1][0])
+        rel_max = max(abs(q - r) / abs(r) for r, q in tl)
+        mae_rel = abs(tm[-1][1] - tm[-1][0]) / abs(tm[-1][0])
+        summ = {
+            "summary": True, "impl": impl, "vs": "torch_fp32", "epochs": a.epochs, "steps": a.epochs * (a.train // b),
+            "image_hw": [h, w], "batch": b, "lr": a.lr,
+            "fp32_loss_first_last": [tl[0][0], tl[-1][0]], "native_loss_first_last": [tl[0][1], tl[-1][1]],
+            "fp32_mae_init_last": [tm[0][0], tm[-1][0]], "native_mae_init_last": [tm[0][1], tm[-1][1]],
+            "loss_gap_last_rel": rel_last, "max_rel_loss_gap": rel_max,
+            "max_abs_mae_gap": max(abs(q - r) for r, q in tm), "mae_gap_last": tm[-1][1] - tm[-1][0],
+            "mae_gap_last_rel": mae_rel,
+            "tolerances": {"mae_last_rel": a.tol_mae_rel, "loss_last_rel": a.tol_loss_last_rel,
+                           "loss_max_rel": a.tol_loss_max_rel},
+            "within_tolerance": bool(mae_rel <= a.tol_mae_rel and rel_last <= a.tol_loss_last_rel and
+                                     rel_max <= a.tol_loss_max_rel),
+        }
+        out.write(json.dumps(summ) + "\n")
+        print(json.dumps(summ), flush=True)
 
 
 if __name__ == "__main__":

@@ -21,8 +21,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _asan_child(code: str, timeout: int = 240):
     from can_distributed_pytorch_amd import build_native as B
-    if not os.path.exists(B.ext_path(asan=True)):
-        B.build(jobs=min(8, os.cpu_count() or 1), asan=True)
+    # incremental: recompiles only the units whose sources changed (the module refuses a stale source hash)
+    B.build(jobs=min(8, os.cpu_count() or 1), asan=True)
     r = subprocess.run([sys.executable, "-c", code], env=B.asan_env(), cwd=ROOT, capture_output=True, text=True,
                        timeout=timeout)
     assert r.returncode == 0, f"rc={r.returncode}\n{r.stdout[-3000:]}\n{r.stderr[-6000:]}"
