@@ -74,7 +74,7 @@ def source_hash(files=None) -> str:
 
 
 def extra_flags():
-    # CANNET_EXTRA_HIPFLAGS: extra defines for A/B variant builds (scripts/gpu/ab_variant_build.sh), e.g.
+    # CANNET_EXTRA_HIPFLAGS: extra defines for A/B variant builds (scripts/dev/ab_variant_build.sh), e.g.
     # -DCANNET_DMA_ORDER_WG=0.  Objects of a flagged build live in their own directory (build/native_<hash>), so
     # setting or clearing the variable never mixes variant objects into the default build.
     return os.environ.get("CANNET_EXTRA_HIPFLAGS", "").split()

@@ -15,7 +15,7 @@ int can_conv_igemm(const void* x, const void* w, const float* bias, const void* 
                    float* bpart, int bpart_cap, int* bpart_rows);
 
 int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, int target_blocks, int* S_out, int* mslice_out,
-                   int* cfg_out, int dil);
+                   int* cfg_out, int dil, int W);
 int can_conv_wgrad(const void* dy, const void* x, float* ws, float* wsb, float* dw, float* db, int N, int H, int W,
                    int Cin, int Cout, int ksize, int dil, int first, int S, int mslice, int cfg, float beta,
                    float scale, const float* dscale, int dt, void* stream, const float* bext, int bext_rows);

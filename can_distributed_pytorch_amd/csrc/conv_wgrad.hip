@@ -852,6 +852,8 @@ static int launch_wgrad3(const WgradArgs2& a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+#include "wgrad_tap.inc"
+
 // ===========================================================================
 // Halo-tiled weight gradient for 3x3 / dilation-1 layers with Cin % 64 == 0 and
 // Cout in {64, 128} (the high-resolution VGG layers conv1_2, conv2_1, conv2_2).
@@ -1271,7 +1273,7 @@ static void wgrad_tile(int cfg, int* TCo, int* TK, int* BKM) {
 }
 
 extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, int target_blocks, int* S_out,
-                              int* mslice_out, int* cfg_out, int dil) {
+                              int* mslice_out, int* cfg_out, int dil, int W) {
   const int K = first ? 64 : ksize * ksize * Cin;
   int cfg;
   // the halo weight-gradient kernel is dilation-1 only (B5: 256 -> 128, dil 2, reaches M >= 262144 at batch 32)
@@ -1289,6 +1291,33 @@ extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, in
   else if (Cout % 128 == 0) cfg = 1;
   else if (K >= 128) cfg = 3;
   else cfg = 4;
+  // the tap-ring kernel (wgrad_tap.inc) for the layers the v2 GEMM takes (dispatch wgrad_tap >= 1) and the Cout = 128
+  // ones of the full-resolution ring kernel (>= 2); it needs the map width (W = 0: unknown, not chosen)
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+      ncu = 256;
+  }
+  // the smallest slice count that fills whole rounds of one-block-per-CU launches to >= 90 %
+  auto whole_rounds = [&](int ntile) {
+    for (int R = 1; R <= 8; ++R) {
+      const int s = (ncu * R) / ntile;
+      if (s >= 1 && (long long)ntile * s * 10 >= 9LL * ncu * R) return s;
+    }
+    return 0;
+  };
+  if (!first && W > 0 && M % W == 0 && wgrad_tap_ok(1, M / W, W, Cin, Cout, ksize, dil) &&
+      g_dispatch.wgrad_tap >= (cfg == 8 ? 2 : 1) && cfg != 0 && (cfg != 8 || Cout == 128)) {
+    const int ntile = (Cin / 64) * (Cout / TAP_TCO);
+    const int stages = (M / W) * ((W + 63) / 64);
+    int S = whole_rounds(ntile);
+    if (S < 1) S = max(1, ncu / ntile);
+    if (S > stages) S = stages;
+    *S_out = S; *mslice_out = 0; *cfg_out = 12;
+    return 0;
+  }
   int TCo, TK, BKM;
   wgrad_tile(cfg, &TCo, &TK, &BKM);
   if (cfg == 8) {
@@ -1307,17 +1336,8 @@ extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, in
     // the pipelined kernels run one block per CU (LDS ring >= 128 KB): as few pixel slices as fill
     // whole rounds of the CUs to >= 90 % (fewer fp32 partial slabs to write and
     // reduce, longer K loops per block)
-    static int ncu = 0;
-    if (!ncu) {
-      int dev = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-        ncu = 256;
-    }
-    for (int R = 1; R <= 8; ++R) {
-      const int s = (ncu * R) / ntile;
-      if (s >= 1 && (long long)ntile * s * 10 >= 9LL * ncu * R) { S = s; break; }
-    }
+    const int wr = whole_rounds(ntile);
+    if (wr) S = wr;
   }
   if (S < 1) S = 1;
   const int max_s = (M + BKM - 1) / BKM;
@@ -1383,7 +1403,7 @@ static int conv_wgrad_impl(const void* dy, const void* x, float* ws, float* wsb,
     a.Ktot = 64; a.S = S; a.mslice = mslice;
     rc = launch_wgrad<DT, 1, 1, 4, true>(a, s);
   } else {
-    if (Cin % 64 || Cout % 64 || H < 2 || W < 2) return -3;
+    if (Cin % 64 || Cout % 64 || ((H < 2 || W < 2) && cfg != 12)) return -3;
     WgradArgs2 a;
     a.dy = (const bf16_t*)dy; a.x = (const bf16_t*)x; a.zero = zero_page(); a.ws = ws; a.wsb = wsb_used;
     if (!a.zero) return -7;
@@ -1398,6 +1418,27 @@ static int conv_wgrad_impl(const void* dy, const void* x, float* ws, float* wsb,
     if (rw) {
       gv.M = N * H * a.tx64 * 64;
       gv.mslice = ((gv.M + S - 1) / S + 63) / 64 * 64;   // slices past the end run no stage and write zero slabs
+    }
+    if (cfg == 12) {
+      if (!wgrad_tap_ok(N, H, W, Cin, Cout, ksize, dil)) return -6;
+      if (wsb_used) {
+        Sb = kBiasParts;
+        hipLaunchKernelGGL(bias_colsum_kernel<DT>, dim3(Sb), dim3(256), 0, s, a.dy, wsb_used, a.M, Cout, Sb);
+      }
+      TapArgs t;
+      t.dy = a.dy; t.x = a.x; t.ws = ws;
+      t.N = N; t.H = H; t.W = W; t.Cin = Cin; t.Cout = Cout;
+      t.tx64 = (W + 63) / 64;
+      t.total = N * H * t.tx64;
+      t.S = S;
+      t.spb = (t.total + S - 1) / S;
+      t.dy_bytes = (unsigned)((long long)a.M * Cout * 2);
+      t.x_bytes = (unsigned)((long long)a.M * Cin * 2);
+      rc = (dil == 1) ? launch_wgrad_tap<DT, 1>(t, s) : launch_wgrad_tap<DT, 2>(t, s);
+      if (rc) return rc;
+      bias_pre();
+      return ext ? launch_reduce2(ws, bsrc, dw, db, S, Sb_ext, K, Cout, Cin, 9, 0, beta, scale, dscale, s)
+                 : launch_reduce2(ws, wsb_used, dw, db, S, Sb, K, Cout, Cin, 9, 0, beta, scale, dscale, s);
     }
     if (cfg == 8) {
       if (ksize != 3 || dil != 1 || (Cout != 64 && Cout != 128) || Cin % 64) return -6;

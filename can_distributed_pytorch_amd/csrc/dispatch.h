@@ -20,6 +20,7 @@ struct DispatchConfig {
   int ring_fast = 1;        // row-ring weight gradient: in-image fast addressing when the shape allows it
   int ring_skew = 1;        // row-ring weight gradient: skewed DMA issue across waves
   int reduce_tiled = 1;     // slab reduction: tiled kernel where it applies (0: grid-stride kernel)
+  int wgrad_tap = 0;        // tap-ring weight gradient (cfg 12): 0 off, 1 the v2-GEMM layers, 2 + the Cout-128 ring ones
 };
 
 // the process-wide configuration (defined in bindings.cpp)

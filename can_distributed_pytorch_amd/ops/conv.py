@@ -277,9 +277,11 @@ class WgradWorkspace:
         self.target_blocks = target_blocks
         self.buf = torch.empty(0, dtype=torch.float32, device=self.device)
 
-    def plan(self, m: int, ci: int, co: int, ksize: int, first: bool, dil: int = 1):
+    def plan(self, m: int, ci: int, co: int, ksize: int, first: bool, dil: int = 1, w: int = 0):
+        """(slices, pixels per slice, kernel config, workspace floats) of one weight gradient; w (the map width, 0 =
+        unknown) lets the planner pick the width-dependent tap-ring kernel."""
         C = _ext.require()
-        s, mslice, cfg = C.wgrad_plan(m, ci, co, ksize, int(first), self.target_blocks, dil)
+        s, mslice, cfg = C.wgrad_plan(m, ci, co, ksize, int(first), self.target_blocks, dil, w)
         ktot = 64 if first else ksize * ksize * ci
         need = s * ktot * co + max(s, 512) * co      # slabs + bias partials (v2 path: 512 column-sum parts)
         return s, mslice, cfg, need
@@ -330,7 +332,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, db: Optional
                        first=first, ws=ws, beta=beta if c == 0 else 1.0, scale=scale, dscale=dscale,
                        bias_partials=bias_partials if c == 0 else None)
         return
-    s, mslice, cfg, need = ws.plan(n * h * w, ci, co, ksize, first, dil)
+    s, mslice, cfg, need = ws.plan(n * h * w, ci, co, ksize, first, dil, w)
     buf = ws.reserve(need)
     ktot = 64 if first else ksize * ksize * ci
     wsb_ptr = buf.data_ptr() + 4 * s * ktot * co

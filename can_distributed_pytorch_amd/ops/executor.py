@@ -184,12 +184,12 @@ class CANNetExecutor:
         need = 0
         hh, ww = h, w
         for s in self.front:
-            _, _, _, nd = self.ws.plan(n * hh * ww, 4 if s.first else s.cin, s.cout, 3, s.first)
+            _, _, _, nd = self.ws.plan(n * hh * ww, 4 if s.first else s.cin, s.cout, 3, s.first, 1, ww)
             need = max(need, nd)
             if s.pool_after:
                 hh, ww = hh // 2, ww // 2
         for s in self.back:
-            need = max(need, self.ws.plan(n * hh * ww, s.cin, s.cout, 3, False, s.dil)[3])
+            need = max(need, self.ws.plan(n * hh * ww, s.cin, s.cout, 3, False, s.dil, ww)[3])
         need = max(need, self.ws.plan(n * hh * ww, 512, 512, 1, False)[3])
         need = max(need, self.ws.plan(n * hh * ww, 512, 4 * 512, 1, False)[3])    # linearised context dW2cat
         need = max(need, max(C.wgrad_1x1_batched_plan(n * hh * ww, 4, 512, 512, ncu=c)[2] for c in (128, 192, 224, 256)))

@@ -133,6 +133,37 @@ def test_conv_wgrad_v2_row_aligned(n, h, w, ci, co, dil, bias):
         _close(db, gb)
 
 
+@pytest.mark.parametrize("n,h,w,ci,co,dil,dtype", [
+    (1, 6, 64, 64, 128, 1, torch.bfloat16), (2, 7, 128, 128, 256, 1, torch.bfloat16),
+    (1, 9, 120, 256, 128, 2, torch.bfloat16), (2, 5, 200, 64, 256, 2, torch.float16),
+    (1, 12, 96, 512, 512, 2, torch.bfloat16), (3, 4, 64, 128, 128, 1, torch.float16),
+    (1, 1, 64, 64, 128, 1, torch.bfloat16), (1, 3, 40, 64, 128, 2, torch.bfloat16),
+    # 1024 -> 512: 64 tiles, 4 slices over 36 stages -> slices that span chains (several segments each)
+    (2, 9, 128, 1024, 512, 2, torch.bfloat16)])
+def test_wgrad_tap_ring(n, h, w, ci, co, dil, dtype, dispatch_cfg):
+    """Tap-ring weight gradient (cfg 12: 128 output channels x 9 taps of a 64-channel input slice, input rows in an
+    LDS ring walked down 64-column chains, one chain per row phase for dilation 2) == the fp32 reference: ragged
+    widths (W % 64 != 0) and heights, single-row maps, slices spanning several chains, bias through the column-sum
+    path."""
+    from can_distributed_pytorch_amd.ops import _ext
+    from can_distributed_pytorch_amd.ops import conv as C
+    dispatch_cfg(wgrad_tap=2)
+    assert _ext.require().wgrad_plan(n * h * w, ci, co, 3, 0, 1024, dil, w)[2] == 12
+    torch.manual_seed(16)
+    x = torch.randn(n, h, w, ci, device="cuda").to(dtype)
+    dy = torch.randn(n, h, w, co, device="cuda").to(dtype)
+    dw = torch.empty(co, ci, 3, 3, device="cuda")
+    db = torch.empty(co, device="cuda")
+    C.conv_wgrad(dy, x, dw, db, ksize=3, dil=dil)
+    torch.cuda.synchronize()
+    wr = torch.zeros(co, ci, 3, 3, device="cuda", requires_grad=True)
+    br = torch.zeros(co, device="cuda", requires_grad=True)
+    y = F.conv2d(x.float().permute(0, 3, 1, 2), wr, br, padding=dil, dilation=dil)
+    gw, gb = torch.autograd.grad(y, (wr, br), dy.float().permute(0, 3, 1, 2))
+    _close(dw, gw)
+    _close(db, gb)
+
+
 def test_conv_wgrad_first_layer():
     from can_distributed_pytorch_amd.ops import conv as C
     torch.manual_seed(4)
