@@ -187,18 +187,6 @@ __device__ __forceinline__ int perm_row(int rho) {
 #define CANNET_DMA_ORDER_WG 2
 #endif
 
-// Wave priority around MFMA bursts (-DCANNET_SETPRIO=1, A/B builds): a wave issuing its MFMA group is raised so its
-// next MFMA is not queued behind the other wave's LDS reads / DMA issue on the same SIMD (the 8-phase GEMM template's
-// s_setprio bracket, cdna_hip_programming.md §5).
-#ifndef CANNET_SETPRIO
-#define CANNET_SETPRIO 0
-#endif
-__device__ __forceinline__ void mfma_prio_hi() {
-  if constexpr (CANNET_SETPRIO != 0) __builtin_amdgcn_s_setprio(1);
-}
-__device__ __forceinline__ void mfma_prio_lo() {
-  if constexpr (CANNET_SETPRIO != 0) __builtin_amdgcn_s_setprio(0);
-}
 
 // ---------------------------------------------------------------------------
 // LDS-DMA through inline asm.  With the __builtin_amdgcn_{global,raw_ptr_buffer}_load_lds builtins hipcc (ROCm

@@ -1070,13 +1070,11 @@ __global__ void __launch_bounds__(64 * WC * WP, 1) conv_glds2_kernel(ConvArgs2 a
   };
   // MFMAs over pixel fragments [i0, i1) (so the B fragments die in halves)
   auto mma = [&](const frag8_t (&af)[JW], const frag8_t (&bfr)[4 * PW], int i0, int i1) {
-    mfma_prio_hi();
 #pragma unroll
     for (int i = i0; i < i1; ++i)
 #pragma unroll
       for (int j = 0; j < JW; ++j)
         acc[j >> 2][j & 3][i] = mfma16<DT>(af[j], bfr[i], acc[j >> 2][j & 3][i]);
-    mfma_prio_lo();
   };
 
   frag8_t a0[JW], b0[4 * PW], a1[JW], b1[4 * PW];
@@ -1377,12 +1375,10 @@ __global__ void __launch_bounds__(512, 1) conv_rring_kernel(ConvArgs2 a) {
       bfr[i] = __builtin_bit_cast(frag8_t, *reinterpret_cast<const uint4*>(base + i * 2048));
   };
   auto mma = [&](const frag8_t (&af)[4], const frag8_t (&bfr)[4 * PW], int i0, int i1) {
-    mfma_prio_hi();
 #pragma unroll
     for (int i = i0; i < i1; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[j][i] = mfma16<DT>(af[j], bfr[i], acc[j][i]);
-    mfma_prio_lo();
   };
 
   frag8_t a0[4], b0[4 * PW], a1[4], b1[4 * PW];

@@ -702,13 +702,11 @@ __global__ void __launch_bounds__(64 * WC * WK, 1) wgrad_glds2_kernel(WgradArgs2
     for (int i = 0; i < 4 * KW; ++i) bfr[i] = rd(Bb, RBB >= 256, RBB, prow0, wk * 64 * KW + i * 16);
   };
   auto mma = [&](const frag8_t (&af)[4], const frag8_t (&bfr)[4 * KW], int i0, int i1) {
-    mfma_prio_hi();
 #pragma unroll
     for (int i = i0; i < i1; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[j][i] = mfma16<DT>(af[j], bfr[i], acc[j][i]);
-    mfma_prio_lo();
   };
 
   if (nstage > 0) {

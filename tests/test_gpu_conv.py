@@ -113,11 +113,13 @@ def test_conv_wgrad(n, h, w, ci, co, k, dil):
     # ragged widths (W % 64 != 0, odd H): virtual 64-pixel stages per row, the padding pixels read zeros
     (2, 7, 100, 256, 256, 1, True), (1, 9, 120, 512, 256, 2, True), (3, 5, 30, 256, 512, 1, False),
     (1, 4, 135, 1024, 512, 2, True)])
-def test_conv_wgrad_v2_row_aligned(n, h, w, ci, co, dil, bias):
-    """W % 64 == 0, Cin % 256 == 0 layers take the v2 pipelined wgrad (cfg 9) with bias column-sum blocks."""
+def test_conv_wgrad_v2_row_aligned(n, h, w, ci, co, dil, bias, dispatch_cfg):
+    """W % 64 == 0, Cin % 256 == 0 layers take the v2 pipelined wgrad (cfg 9) with bias column-sum blocks (with the
+    tap-ring kernel off: it takes these layers by default)."""
     from can_distributed_pytorch_amd.ops import _ext
     from can_distributed_pytorch_amd.ops import conv as C
-    assert _ext.require().wgrad_plan(n * h * w, ci, co, 3, 0, 1024)[2] == 9
+    dispatch_cfg(wgrad_tap=0)
+    assert _ext.require().wgrad_plan(n * h * w, ci, co, 3, 0, 1024, dil, w)[2] == 9
     torch.manual_seed(6)
     x = torch.randn(n, h, w, ci, device="cuda").to(torch.bfloat16)
     dy = torch.randn(n, h, w, co, device="cuda").to(torch.bfloat16)
@@ -189,8 +191,8 @@ def test_conv_wgrad_halo_path(n, h, w, ci, co, ring, dispatch_cfg):
     cross strip boundaries (full-halo reload mid-slice) and a ragged last tile row."""
     from can_distributed_pytorch_amd.ops import _ext
     from can_distributed_pytorch_amd.ops import conv as C
-    dispatch_cfg(wgrad_halo_ring=int(ring))
-    assert _ext.require().wgrad_plan(n * h * w, ci, co, 3, 0, 1024)[2] == 8
+    dispatch_cfg(wgrad_halo_ring=int(ring), wgrad_tap=0)
+    assert _ext.require().wgrad_plan(n * h * w, ci, co, 3, 0, 1024, 1, w)[2] == 8
     torch.manual_seed(5)
     x = torch.randn(n, h, w, ci, device="cuda").to(torch.bfloat16)
     dy = torch.randn(n, h, w, co, device="cuda").to(torch.bfloat16)
@@ -213,7 +215,8 @@ def test_ring_wgrad_fast_addressing_bitwise(n, h, w, ci, co, dtype, dispatch_cfg
     bitwise: several strips per image, several images, 2 ci / co tiles, slices crossing strips."""
     from can_distributed_pytorch_amd.ops import _ext
     from can_distributed_pytorch_amd.ops import conv as C
-    assert _ext.require().wgrad_plan(n * h * w, ci, co, 3, 0, 1024)[2] == 8
+    dispatch_cfg(wgrad_tap=0)
+    assert _ext.require().wgrad_plan(n * h * w, ci, co, 3, 0, 1024, 1, w)[2] == 8
     torch.manual_seed(21)
     x = torch.randn(n, h, w, ci, device="cuda").to(dtype)
     dy = torch.randn(n, h, w, co, device="cuda").to(dtype)
@@ -261,11 +264,13 @@ def test_conv_wgrad_1x1_batched(dtype):
     (2, 4, 64, 512, 128, 1, 11, True),
     # ragged widths (W % 64 != 0): virtual 64-pixel stages per row, padding pixels zero
     (1, 6, 90, 128, 256, 1, 10, True), (2, 5, 100, 512, 128, 2, 11, True)])
-def test_conv_wgrad_v2_half_tiles(n, h, w, ci, co, dil, cfg, bias):
-    """v2 pipelined wgrad with 256co x 128k (Cin = 128, cfg 10) and 128co x 256k (Cout = 128, cfg 11) tiles."""
+def test_conv_wgrad_v2_half_tiles(n, h, w, ci, co, dil, cfg, bias, dispatch_cfg):
+    """v2 pipelined wgrad with 256co x 128k (Cin = 128, cfg 10) and 128co x 256k (Cout = 128, cfg 11) tiles (tap-ring
+    kernel off)."""
     from can_distributed_pytorch_amd.ops import _ext
     from can_distributed_pytorch_amd.ops import conv as C
-    assert _ext.require().wgrad_plan(n * h * w, ci, co, 3, 0, 1024)[2] == cfg
+    dispatch_cfg(wgrad_tap=0)
+    assert _ext.require().wgrad_plan(n * h * w, ci, co, 3, 0, 1024, dil, w)[2] == cfg
     torch.manual_seed(8)
     x = torch.randn(n, h, w, ci, device="cuda").to(torch.bfloat16)
     dy = torch.randn(n, h, w, co, device="cuda").to(torch.bfloat16)
