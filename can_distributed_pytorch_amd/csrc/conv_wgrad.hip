@@ -1432,7 +1432,10 @@ static int conv_wgrad_impl(const void* dy, const void* x, float* ws, float* wsb,
       t.spb = (t.total + S - 1) / S;
       t.dy_bytes = (unsigned)((long long)a.M * Cout * 2);
       t.x_bytes = (unsigned)((long long)a.M * Cin * 2);
-      rc = (dil == 1) ? launch_wgrad_tap<DT, 1>(t, s) : launch_wgrad_tap<DT, 2>(t, s);
+      if (g_dispatch.wgrad_tap_adb)
+        rc = (dil == 1) ? launch_wgrad_tap<DT, 1, true>(t, s) : launch_wgrad_tap<DT, 2, true>(t, s);
+      else
+        rc = (dil == 1) ? launch_wgrad_tap<DT, 1, false>(t, s) : launch_wgrad_tap<DT, 2, false>(t, s);
       if (rc) return rc;
       bias_pre();
       return ext ? launch_reduce2(ws, bsrc, dw, db, S, Sb_ext, K, Cout, Cin, 9, 0, beta, scale, dscale, s)
