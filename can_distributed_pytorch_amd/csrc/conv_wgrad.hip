@@ -1306,12 +1306,19 @@ extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, in
     }
     return 0;
   };
-  if (!first && W > 0 && M % W == 0 && wgrad_tap_ok(1, M / W, W, Cin, Cout, ksize, dil) &&
-      g_dispatch.wgrad_tap >= (cfg == 8 ? 2 : 1) && cfg != 0 && (cfg != 8 || Cout == 128)) {
-    const int ntile = (Cin / 64) * (Cout / TAP_TCO);
+  const int tco = wgrad_tap_tco(Cout);
+  if (!first && W > 0 && M % W == 0 && wgrad_tap_ok(1, M / W, W, Cin, Cout, ksize, dil) && cfg != 0 &&
+      g_dispatch.wgrad_tap >= (tco == 64 ? 3 : cfg == 8 ? 2 : 1)) {
+    // one block per CU (TCO 128) or two (TCO 64)
+    const int ntile = (Cin / 64) * (Cout / tco);
     const int stages = (M / W) * ((W + 63) / 64);
-    int S = whole_rounds(ntile);
-    if (S < 1) S = max(1, ncu / ntile);
+    const int slots_per_cu = (tco == 128) ? 1 : 2;
+    int S = 0;
+    for (int R = 1; R <= 8 && !S; ++R) {
+      const int s = (ncu * slots_per_cu * R) / ntile;
+      if (s >= 1 && (long long)ntile * s * 10 >= 9LL * ncu * slots_per_cu * R) S = s;
+    }
+    if (S < 1) S = max(1, ncu * slots_per_cu / ntile);
     if (S > stages) S = stages;
     *S_out = S; *mslice_out = 0; *cfg_out = 12;
     return 0;
@@ -1432,10 +1439,14 @@ static int conv_wgrad_impl(const void* dy, const void* x, float* ws, float* wsb,
       t.spb = (t.total + S - 1) / S;
       t.dy_bytes = (unsigned)((long long)a.M * Cout * 2);
       t.x_bytes = (unsigned)((long long)a.M * Cin * 2);
-      if (g_dispatch.wgrad_tap_adb)
-        rc = (dil == 1) ? launch_wgrad_tap<DT, 1, true>(t, s) : launch_wgrad_tap<DT, 2, true>(t, s);
-      else
-        rc = (dil == 1) ? launch_wgrad_tap<DT, 1, false>(t, s) : launch_wgrad_tap<DT, 2, false>(t, s);
+      const bool adb = g_dispatch.wgrad_tap_adb != 0;
+      if (wgrad_tap_tco(Cout) == 128) {
+        if (adb) rc = (dil == 1) ? launch_wgrad_tap<DT, 1, 128, true>(t, s) : launch_wgrad_tap<DT, 2, 128, true>(t, s);
+        else rc = (dil == 1) ? launch_wgrad_tap<DT, 1, 128, false>(t, s) : launch_wgrad_tap<DT, 2, 128, false>(t, s);
+      } else {
+        if (adb) rc = (dil == 1) ? launch_wgrad_tap<DT, 1, 64, true>(t, s) : launch_wgrad_tap<DT, 2, 64, true>(t, s);
+        else rc = (dil == 1) ? launch_wgrad_tap<DT, 1, 64, false>(t, s) : launch_wgrad_tap<DT, 2, 64, false>(t, s);
+      }
       if (rc) return rc;
       bias_pre();
       return ext ? launch_reduce2(ws, bsrc, dw, db, S, Sb_ext, K, Cout, Cin, 9, 0, beta, scale, dscale, s)

@@ -31,7 +31,8 @@ class DispatchConfig:
     ring_fast: int = 1        # row-ring weight gradient: fast in-image addressing where the shape allows
     ring_skew: int = 1        # row-ring weight gradient: skewed DMA issue
     reduce_tiled: int = 1     # slab reduction: tiled kernel where it applies
-    wgrad_tap: int = 2        # tap-ring weight gradient (cfg 12): 0 off, 1 v2-GEMM layers, 2 + Cout-128 ring layers
+    wgrad_tap: int = 2        # tap-ring weight gradient (cfg 12): 0 off, 1 v2-GEMM layers, 2 + Cout-128 ring layers,
+    #                           3 + Cout-64 layers
     wgrad_tap_adb: int = 0    # tap ring: double-buffered dY fragments (A/B)
     # ---- executor / front-end (Python)
     w1g: int = 1              # conv1_1's weight gradient fused into conv1_2's data gradient
@@ -53,7 +54,7 @@ class DispatchConfig:
 _ALLOWED = {
     "rring": (0, 1, 2), "rring64": (0, 1), "rring128": (0, 1, 2, 3), "ws64": (0, 1), "ctx_tile_f": (128, 256),
     "ctx_tile_b": (128, 256), "wgrad_halo_ring": (0, 1), "ring_fast": (0, 1), "ring_skew": (0, 1),
-    "reduce_tiled": (0, 1), "wgrad_tap": (0, 1, 2), "wgrad_tap_adb": (0, 1), "w1g": (0, 1), "pool_fwd_fused": (0, 1), "poolbwd_fused": (0, 1), "ctx_linear": (0, 1),
+    "reduce_tiled": (0, 1), "wgrad_tap": (0, 1, 2, 3), "wgrad_tap_adb": (0, 1), "w1g": (0, 1), "pool_fwd_fused": (0, 1), "poolbwd_fused": (0, 1), "ctx_linear": (0, 1),
     "ctx_batched": (0, 1), "bias_fused": (0, 1), "wgrad_stream": (0, 1),
 }
 

@@ -9,10 +9,12 @@ grep -q " passed" gpurun_out/tap_tests.log && ! grep -q "failed\|error" gpurun_o
 for r in 1 2; do
   $S wconv_base_$r 300 python scripts/bench_convs.py --no-ref --passes wgrad --iters 20 || exit $?
   CANNET_DISPATCH=wgrad_tap_adb=1 $S wconv_adb_$r 300 python scripts/bench_convs.py --no-ref --passes wgrad --iters 20 || exit $?
+  CANNET_DISPATCH=wgrad_tap=3 $S wconv_tap3_$r 300 python scripts/bench_convs.py --no-ref --passes wgrad --iters 20 || exit $?
 done
 for r in 1 2 3; do
   $S step_base_$r 300 python bench.py --steps 30 --warmup 5 || exit $?
   CANNET_DISPATCH=wgrad_tap_adb=1 $S step_adb_$r 300 python bench.py --steps 30 --warmup 5 || exit $?
+  CANNET_DISPATCH=wgrad_tap=3 $S step_tap3_$r 300 python bench.py --steps 30 --warmup 5 || exit $?
 done
 for q in 1 2 4; do
   DEBUG_HIP_FORCE_GRAPH_QUEUES=$q $S graph_q$q 300 python bench.py --steps 30 --warmup 5 --graph 1 || exit $?

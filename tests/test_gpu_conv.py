@@ -141,7 +141,10 @@ def test_conv_wgrad_v2_row_aligned(n, h, w, ci, co, dil, bias, dispatch_cfg):
     (1, 12, 96, 512, 512, 2, torch.bfloat16), (3, 4, 64, 128, 128, 1, torch.float16),
     (1, 1, 64, 64, 128, 1, torch.bfloat16), (1, 3, 40, 64, 128, 2, torch.bfloat16),
     # 1024 -> 512: 64 tiles, 4 slices over 36 stages -> slices that span chains (several segments each)
-    (2, 9, 128, 1024, 512, 2, torch.bfloat16)])
+    (2, 9, 128, 1024, 512, 2, torch.bfloat16),
+    # Cout = 64: the 64-channel tile (4 waves, two blocks per CU, 2-stage DMA lead)
+    (1, 6, 64, 64, 64, 1, torch.bfloat16), (2, 9, 120, 128, 64, 2, torch.bfloat16),
+    (1, 5, 200, 64, 64, 1, torch.float16), (3, 16, 256, 64, 64, 1, torch.bfloat16)])
 @pytest.mark.parametrize("adb", [0, 1])
 def test_wgrad_tap_ring(n, h, w, ci, co, dil, dtype, adb, dispatch_cfg):
     """Tap-ring weight gradient (cfg 12: 128 output channels x 9 taps of a 64-channel input slice, input rows in an
@@ -150,7 +153,7 @@ def test_wgrad_tap_ring(n, h, w, ci, co, dil, dtype, adb, dispatch_cfg):
     path."""
     from can_distributed_pytorch_amd.ops import _ext
     from can_distributed_pytorch_amd.ops import conv as C
-    dispatch_cfg(wgrad_tap=2, wgrad_tap_adb=adb)
+    dispatch_cfg(wgrad_tap=3, wgrad_tap_adb=adb)
     assert _ext.require().wgrad_plan(n * h * w, ci, co, 3, 0, 1024, dil, w)[2] == 12
     torch.manual_seed(16)
     x = torch.randn(n, h, w, ci, device="cuda").to(dtype)
