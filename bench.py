@@ -191,6 +191,11 @@ def main(argv=None) -> int:
         print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}: refusing to mislabel the run", file=sys.stderr)
         return 2
 
+    if a.graph:
+        # hipGraph replay with ONE graph queue: the runtime default spreads the captured two-stream step over several
+        # queues and resolved fewer concurrent kernels (497.5 vs 513.7 img/s, profiles/r4/graph_queues.txt).  Read
+        # by the HIP runtime at its initialisation, so set before the first GPU call.
+        os.environ.setdefault("DEBUG_HIP_FORCE_GRAPH_QUEUES", "1")
     import torch
     import torch.distributed as dist
     cpu = a.device == "cpu"

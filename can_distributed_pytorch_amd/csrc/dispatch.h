@@ -22,8 +22,8 @@ struct DispatchConfig {
   int reduce_tiled = 1;     // slab reduction: tiled kernel where it applies (0: grid-stride kernel)
   // tap-ring weight gradient (cfg 12): 0 off, 1 the v2-GEMM layers, 2 (default) + the Cout = 128 full-resolution ring
   // ones, 3 + the Cout = 64 layers (64-channel tile, two blocks per CU): step 495.6 -> 511.8 (1) / 516.5 (2) img/s, 3 interleaved rounds (profiles/r4/ab_wgrad_tap.txt)
-  int wgrad_tap = 2;
-  int wgrad_tap_adb = 0;    // tap ring: double-buffered dY fragments (A/B)
+  int wgrad_tap = 3;        // 3: 521.4 vs 518.4 img/s (2), 3 interleaved rounds (profiles/r4/ab_wgrad_tap_variants.txt)
+  int wgrad_tap_adb = 1;    // tap ring: double-buffered dY fragments (step +0.45 %, same file)
 };
 
 // the process-wide configuration (defined in bindings.cpp)

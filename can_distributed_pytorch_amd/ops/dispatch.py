@@ -31,9 +31,9 @@ class DispatchConfig:
     ring_fast: int = 1        # row-ring weight gradient: fast in-image addressing where the shape allows
     ring_skew: int = 1        # row-ring weight gradient: skewed DMA issue
     reduce_tiled: int = 1     # slab reduction: tiled kernel where it applies
-    wgrad_tap: int = 2        # tap-ring weight gradient (cfg 12): 0 off, 1 v2-GEMM layers, 2 + Cout-128 ring layers,
+    wgrad_tap: int = 3        # tap-ring weight gradient (cfg 12): 0 off, 1 v2-GEMM layers, 2 + Cout-128 ring layers,
     #                           3 + Cout-64 layers
-    wgrad_tap_adb: int = 0    # tap ring: double-buffered dY fragments (A/B)
+    wgrad_tap_adb: int = 1    # tap ring: double-buffered dY fragments
     # ---- executor / front-end (Python)
     w1g: int = 1              # conv1_1's weight gradient fused into conv1_2's data gradient
     pool_fwd_fused: int = 1   # 2x2 max-pool in the conv epilogue

@@ -127,6 +127,9 @@ def make_loaders(args, world, rank, raw=False, device=None, dtype=None):
 
 
 def main(args):
+    if args.graph:
+        # one hipGraph queue for the replayed step (bench.py, profiles/r4/graph_queues.txt); read at HIP init
+        os.environ.setdefault("DEBUG_HIP_FORCE_GRAPH_QUEUES", "1")
     init_distributed_mode(args)
     rank, world = args.rank, args.world_size
     use_gpu = str(args.device).startswith("cuda") and torch.cuda.is_available()
