@@ -34,6 +34,7 @@ class DispatchConfig:
     wgrad_tap: int = 3        # tap-ring weight gradient (cfg 12): 0 off, 1 v2-GEMM layers, 2 + Cout-128 ring layers,
     #                           3 + Cout-64 layers
     wgrad_tap_adb: int = 1    # tap ring: double-buffered dY fragments
+    wgrad_tap_ks: int = 0     # tap ring, Cout = 64: 8 waves splitting each stage's pixels
     # ---- executor / front-end (Python)
     w1g: int = 1              # conv1_1's weight gradient fused into conv1_2's data gradient
     pool_fwd_fused: int = 1   # 2x2 max-pool in the conv epilogue
@@ -45,7 +46,7 @@ class DispatchConfig:
     ctx_wgrad_cus: int = 224  # CUs the batched context 1x1 weight gradient is planned for
 
     NATIVE = ("rring", "rring64", "rring128", "ws64", "ctx_tile_f", "ctx_tile_b", "wgrad_halo_ring", "ring_fast",
-              "ring_skew", "reduce_tiled", "wgrad_tap", "wgrad_tap_adb")
+              "ring_skew", "reduce_tiled", "wgrad_tap", "wgrad_tap_adb", "wgrad_tap_ks")
 
     def native(self) -> Dict[str, int]:
         return {k: getattr(self, k) for k in self.NATIVE}
@@ -54,7 +55,7 @@ class DispatchConfig:
 _ALLOWED = {
     "rring": (0, 1, 2), "rring64": (0, 1), "rring128": (0, 1, 2, 3), "ws64": (0, 1), "ctx_tile_f": (128, 256),
     "ctx_tile_b": (128, 256), "wgrad_halo_ring": (0, 1), "ring_fast": (0, 1), "ring_skew": (0, 1),
-    "reduce_tiled": (0, 1), "wgrad_tap": (0, 1, 2, 3), "wgrad_tap_adb": (0, 1), "w1g": (0, 1), "pool_fwd_fused": (0, 1), "poolbwd_fused": (0, 1), "ctx_linear": (0, 1),
+    "reduce_tiled": (0, 1), "wgrad_tap": (0, 1, 2, 3), "wgrad_tap_adb": (0, 1), "wgrad_tap_ks": (0, 1), "w1g": (0, 1), "pool_fwd_fused": (0, 1), "poolbwd_fused": (0, 1), "ctx_linear": (0, 1),
     "ctx_batched": (0, 1), "bias_fused": (0, 1), "wgrad_stream": (0, 1),
 }
 
