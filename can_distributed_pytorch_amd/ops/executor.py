@@ -385,7 +385,10 @@ class CANNetExecutor:
         cur.wait_stream(hi)
 
     def _bwd_stream(self):
-        if not dispatch.current().bwd_priority or self.stream_override is not None:
+        # not inside a hipGraph capture: graph nodes carry no stream priority, and ending a capture that forked onto
+        # a high-priority stream crashed the HIP runtime (host segfault in capture_end, ROCm 7.2)
+        if (not dispatch.current().bwd_priority or self.stream_override is not None
+                or torch.cuda.is_current_stream_capturing()):
             return None
         dev = self.head.weight.device
         if getattr(self, "_hi", None) is None or self._hi.device != dev:

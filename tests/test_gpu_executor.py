@@ -241,7 +241,7 @@ def test_native_stepper_row_ring_matches_per_tap_kernel(mode, dispatch_cfg):
 def test_native_stepper_high_priority_backward_bitwise(graph, dispatch_cfg):
     """dispatch bwd_priority = 1 runs the data-gradient chain on a high-priority stream (the weight-gradient stream
     forks from and joins into it): the same kernels on the same data, so the trained weights are bitwise those of
-    the default schedule, eager and captured in a hipGraph."""
+    the default schedule.  A hipGraph capture keeps the default streams (graph nodes carry no priority)."""
     from can_distributed_pytorch_amd.engine.native import NativeStepper
     _, nat_a = _models(13)
     nat_b = copy.deepcopy(nat_a)
@@ -256,6 +256,6 @@ def test_native_stepper_high_priority_backward_bitwise(graph, dispatch_cfg):
     for _ in range(2):
         b.step(x, gt)
     torch.cuda.synchronize()
-    assert b.ex._hi is not None
+    assert (getattr(b.ex, "_hi", None) is not None) == (not graph)
     for (name, pa), pb in zip(nat_a.named_parameters(), nat_b.parameters()):
         assert torch.equal(pa, pb), name
