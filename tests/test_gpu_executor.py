@@ -256,6 +256,6 @@ def test_native_stepper_high_priority_backward_bitwise(graph, dispatch_cfg):
     for _ in range(2):
         b.step(x, gt)
     torch.cuda.synchronize()
-    assert (getattr(b.ex, "_hi", None) is not None) == (not graph)
+    assert getattr(b.ex, "_hi", None) is not None          # (graph: used by the eager warm-up steps)
     for (name, pa), pb in zip(nat_a.named_parameters(), nat_b.parameters()):
         assert torch.equal(pa, pb), name
