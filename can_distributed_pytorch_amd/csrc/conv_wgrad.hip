@@ -1312,8 +1312,7 @@ extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, in
     // one block per CU (TCO 128) or two (TCO 64)
     const int ntile = (Cin / 64) * (Cout / tco);
     const int stages = (M / W) * ((W + 63) / 64);
-    const bool ks = (tco == 64) && g_dispatch.wgrad_tap_ks;       // pixel-split 8-wave form: one block per CU
-    const int slots_per_cu = (tco == 128 || ks) ? 1 : 2;
+    const int slots_per_cu = (tco == 128) ? 1 : 2;
     int S = 0;
     for (int R = 1; R <= 8 && !S; ++R) {
       const int s = (ncu * slots_per_cu * R) / ntile;
@@ -1321,7 +1320,7 @@ extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, in
     }
     if (S < 1) S = max(1, ncu * slots_per_cu / ntile);
     if (S > stages) S = stages;
-    *S_out = ks ? 2 * S : S; *mslice_out = 0; *cfg_out = 12;        // slabs (two per slice with the pixel split)
+    *S_out = S; *mslice_out = 0; *cfg_out = 12;
     return 0;
   }
   int TCo, TK, BKM;
@@ -1436,19 +1435,14 @@ static int conv_wgrad_impl(const void* dy, const void* x, float* ws, float* wsb,
       t.N = N; t.H = H; t.W = W; t.Cin = Cin; t.Cout = Cout;
       t.tx64 = (W + 63) / 64;
       t.total = N * H * t.tx64;
-      const bool ks = wgrad_tap_tco(Cout) == 64 && g_dispatch.wgrad_tap_ks;
-      if (ks && S % 2) return -6;                                   // planned with the other setting
-      t.S = ks ? S / 2 : S;                                         // slices (slabs: S)
-      t.spb = (t.total + t.S - 1) / t.S;
+      t.S = S;
+      t.spb = (t.total + S - 1) / S;
       t.dy_bytes = (unsigned)((long long)a.M * Cout * 2);
       t.x_bytes = (unsigned)((long long)a.M * Cin * 2);
       const bool adb = g_dispatch.wgrad_tap_adb != 0;
       if (wgrad_tap_tco(Cout) == 128) {
         if (adb) rc = (dil == 1) ? launch_wgrad_tap<DT, 1, 128, true>(t, s) : launch_wgrad_tap<DT, 2, 128, true>(t, s);
         else rc = (dil == 1) ? launch_wgrad_tap<DT, 1, 128, false>(t, s) : launch_wgrad_tap<DT, 2, 128, false>(t, s);
-      } else if (ks) {
-        if (adb) rc = (dil == 1) ? launch_wgrad_tap<DT, 1, 64, true, true>(t, s) : launch_wgrad_tap<DT, 2, 64, true, true>(t, s);
-        else rc = (dil == 1) ? launch_wgrad_tap<DT, 1, 64, false, true>(t, s) : launch_wgrad_tap<DT, 2, 64, false, true>(t, s);
       } else {
         if (adb) rc = (dil == 1) ? launch_wgrad_tap<DT, 1, 64, true>(t, s) : launch_wgrad_tap<DT, 2, 64, true>(t, s);
         else rc = (dil == 1) ? launch_wgrad_tap<DT, 1, 64, false>(t, s) : launch_wgrad_tap<DT, 2, 64, false>(t, s);

@@ -372,30 +372,8 @@ class CANNetExecutor:
         accumulated when beta=1).  Entries for the head must already be filled.
         dscale: optional fp32 device scalar multiplied into every weight gradient
         (1 / loss scale when d_b6 carries a loss scale, fp16 step).
-        dispatch bwd_priority = 1: the data-gradient chain (the step's critical path) runs on a high-priority stream,
-        so its kernels take CUs ahead of the weight-gradient stream's.
+        (A data-gradient chain on a high-priority stream measured neutral: profiles/r4/ab_confirm.txt.)
         """
-        hi = self._bwd_stream()
-        if hi is None:
-            return self._backward_features(sv, d_b6, grads, on_grad_ready, beta, scale, dscale)
-        cur = torch.cuda.current_stream(d_b6.device)
-        hi.wait_stream(cur)
-        with torch.cuda.stream(hi):
-            self._backward_features(sv, d_b6, grads, on_grad_ready, beta, scale, dscale)
-        cur.wait_stream(hi)
-
-    def _bwd_stream(self):
-        # not inside a hipGraph capture: graph nodes carry no stream priority, and ending a capture that forked onto
-        # a high-priority stream crashed the HIP runtime (host segfault in capture_end, ROCm 7.2)
-        if (not dispatch.current().bwd_priority or self.stream_override is not None
-                or torch.cuda.is_current_stream_capturing()):
-            return None
-        dev = self.head.weight.device
-        if getattr(self, "_hi", None) is None or self._hi.device != dev:
-            self._hi = torch.cuda.Stream(dev, priority=-1)
-        return self._hi
-
-    def _backward_features(self, sv, d_b6, grads, on_grad_ready, beta, scale, dscale):
         st = self._stream()
         ws = self.ws or self.workspace(*self._shape_from(sv))
         ready = on_grad_ready or (lambda idx: None)

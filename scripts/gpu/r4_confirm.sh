@@ -11,13 +11,8 @@ for r in 1 2 3; do
   $S step_def_$r 300 python bench.py --steps 30 --warmup 5 || exit $?
   CANNET_DISPATCH=wgrad_tap_adb=0 $S step_noadb_$r 300 python bench.py --steps 30 --warmup 5 || exit $?
   CANNET_DISPATCH=wgrad_tap=2,wgrad_tap_adb=0 $S step_tap2_$r 300 python bench.py --steps 30 --warmup 5 || exit $?
-  CANNET_DISPATCH=wgrad_tap_ks=1 $S step_ks_$r 300 python bench.py --steps 30 --warmup 5 || exit $?
-  CANNET_DISPATCH=bwd_priority=1 $S step_hi_$r 300 python bench.py --steps 30 --warmup 5 || exit $?
+  # (profiles/r4/ab_confirm.txt also has wgrad_tap_ks=1 / bwd_priority=1 arms, run at commit 7a9a511; both removed)
   CANNET_DISPATCH=rring128=2 $S step_r128_$r 300 python bench.py --steps 30 --warmup 5 || exit $?
-done
-for r in 1 2; do
-  $S wconv_def_$r 300 python scripts/bench_convs.py --no-ref --passes wgrad --layers F2,B6 --iters 20 || exit $?
-  CANNET_DISPATCH=wgrad_tap_ks=1 $S wconv_ks_$r 300 python scripts/bench_convs.py --no-ref --passes wgrad --layers F2,B6 --iters 20 || exit $?
 done
 $S b_default 300 python bench.py || exit $?
 $S b_graph 300 python bench.py --steps 30 --warmup 5 --graph 1 || exit $?

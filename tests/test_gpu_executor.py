@@ -236,26 +236,3 @@ def test_native_stepper_row_ring_matches_per_tap_kernel(mode, dispatch_cfg):
         else:
             assert torch.equal(pa, pb), name
 
-
-@pytest.mark.parametrize("graph", [False, True])
-def test_native_stepper_high_priority_backward_bitwise(graph, dispatch_cfg):
-    """dispatch bwd_priority = 1 runs the data-gradient chain on a high-priority stream (the weight-gradient stream
-    forks from and joins into it): the same kernels on the same data, so the trained weights are bitwise those of
-    the default schedule.  A hipGraph capture keeps the default streams (graph nodes carry no priority)."""
-    from can_distributed_pytorch_amd.engine.native import NativeStepper
-    _, nat_a = _models(13)
-    nat_b = copy.deepcopy(nat_a)
-    x = torch.randn(2, 3, 96, 128, device="cuda")
-    gt = torch.rand(2, 1, 12, 16, device="cuda")
-    dispatch_cfg(bwd_priority=0)
-    a = NativeStepper("cuda", lr=1e-4, graph=graph, model=nat_a)
-    for _ in range(2):
-        a.step(x, gt)
-    dispatch_cfg(bwd_priority=1)
-    b = NativeStepper("cuda", lr=1e-4, graph=graph, model=nat_b)
-    for _ in range(2):
-        b.step(x, gt)
-    torch.cuda.synchronize()
-    assert getattr(b.ex, "_hi", None) is not None          # (graph: used by the eager warm-up steps)
-    for (name, pa), pb in zip(nat_a.named_parameters(), nat_b.parameters()):
-        assert torch.equal(pa, pb), name
