@@ -218,7 +218,7 @@ def bias_part_capacity(n: int, h: int, w: int) -> int:
 
 
 def conv_dgrad_with_bias(dy: torch.Tensor, wpack: torch.Tensor, *, ksize: int, dil: int = 1, epi: int = EPI_MASK,
-                         mask: torch.Tensor, tile: int = 0):
+                         mask: torch.Tensor, tile: int = 0, out: Optional[torch.Tensor] = None):
     """Data gradient (EPI_MASK / EPI_POOLBWD) whose epilogue also sums the bias gradient of the gradient it
     writes (the next layer's dY): returns (dX, partials [rows, Cin] fp32 or None when the kernel path does not
     produce them).  conv_wgrad(bias_partials=...) reduces them into db instead of re-reading dY."""
@@ -227,7 +227,7 @@ def conv_dgrad_with_bias(dy: torch.Tensor, wpack: torch.Tensor, *, ksize: int, d
     bp = torch.empty(bias_part_capacity(n, h, w), co, dtype=torch.float32, device=dy.device)
     # long partial lists are folded by conv_wgrad on the weight-gradient stream after its GEMM (folded here, on the
     # producer's critical-path stream, the short launch waited 85-345 us for CUs, profiles/r3/ab_bias_prereduce.txt)
-    return conv_igemm(dy, wpack, None, ksize=ksize, dil=dil, epi=epi, mask=mask, tile=tile, bias_part=bp)
+    return conv_igemm(dy, wpack, None, ksize=ksize, dil=dil, epi=epi, mask=mask, tile=tile, bias_part=bp, out=out)
 
 
 def _check_codes(codes: Optional[torch.Tensor], pooled_shape) -> None:

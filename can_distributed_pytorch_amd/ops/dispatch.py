@@ -42,6 +42,7 @@ class DispatchConfig:
     ctx_batched: int = 1      # direct form: the four conv{S}_2 convs in one launch
     bias_fused: int = 1       # bias gradients from the data-gradient epilogue partials
     wgrad_stream: int = 1     # weight gradients on a second stream
+    tail_split: int = 0       # conv2_1 dgrad / conv1_2 wgrad in image halves (overlap the step's tail; A/B)
     ctx_wgrad_cus: int = 224  # CUs the batched context 1x1 weight gradient is planned for
 
     NATIVE = ("rring", "rring64", "rring128", "ws64", "ctx_tile_f", "ctx_tile_b", "wgrad_halo_ring", "ring_fast",
@@ -55,7 +56,7 @@ _ALLOWED = {
     "rring": (0, 1, 2), "rring64": (0, 1), "rring128": (0, 1, 2, 3), "ws64": (0, 1), "ctx_tile_f": (128, 256),
     "ctx_tile_b": (128, 256), "wgrad_halo_ring": (0, 1), "ring_fast": (0, 1), "ring_skew": (0, 1),
     "reduce_tiled": (0, 1), "wgrad_tap": (0, 1, 2, 3), "wgrad_tap_adb": (0, 1), "w1g": (0, 1), "pool_fwd_fused": (0, 1), "poolbwd_fused": (0, 1), "ctx_linear": (0, 1),
-    "ctx_batched": (0, 1), "bias_fused": (0, 1), "wgrad_stream": (0, 1),
+    "ctx_batched": (0, 1), "bias_fused": (0, 1), "wgrad_stream": (0, 1), "tail_split": (0, 1),
 }
 
 

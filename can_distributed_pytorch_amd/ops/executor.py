@@ -387,13 +387,16 @@ class CANNetExecutor:
         # profiles/r3/ab_bias_fused.txt), so it is the default; dispatch bias_fused = 0 re-reads dY
         fuse_bias = bool(dispatch.current().bias_fused)
 
-        def wg(spec_or_w, dy, x, ksize, dil, first, wi, bi, bp=None):
+        def wg(spec_or_w, dy, x, ksize, dil, first, wi, bi, bp=None, wbeta=None, mark=True):
             # bp: bias partials of dy summed by the data-gradient epilogue that wrote it (None: the weight-
-            # gradient launch re-reads dy for the bias)
+            # gradient launch re-reads dy for the bias); wbeta / mark: a later image chunk accumulates (beta 1) and
+            # only the last one marks the gradient ready
             def run():
                 C.conv_wgrad(dy, x, grads[wi], grads[bi] if bi is not None else None, ksize=ksize, dil=dil,
-                             first=first, ws=ws, beta=beta, scale=scale, dscale=dscale, bias_partials=bp)
-                ready([wi] + ([bi] if bi is not None else []))
+                             first=first, ws=ws, beta=beta if wbeta is None else wbeta, scale=scale, dscale=dscale,
+                             bias_partials=bp)
+                if mark:
+                    ready([wi] + ([bi] if bi is not None else []))
             self._on_side(side, run, hold, dy, x, *(() if bp is None else (bp,)))
 
         def dgrad(dy, dgr, dil, epi, mask):
@@ -416,9 +419,11 @@ class CANNetExecutor:
         dy = self._context_bwd(sv["ctx"], sv["fv"], dcat, grads, ws, beta, scale, ready, dscale, side, hold)
         # ---- frontend, reverse
         bp = None
+        wg_done = set()          # layers whose weight gradient already ran (image halves, tail_split)
         for s in reversed(self.front):
             x = sv["front_in"][s.idx]
-            wg(s, dy, x, 3, 1, s.first, s.w_index, s.b_index, bp)
+            if s.idx not in wg_done:
+                wg(s, dy, x, 3, 1, s.first, s.w_index, s.b_index, bp)
             if s.idx == 0:
                 break
             _, dgr = self.packs[id(s.module.weight)]
@@ -441,7 +446,28 @@ class CANNetExecutor:
                 # (+ ReLU mask of the pool input) in the conv epilogue: the pooled gradient never
                 # round-trips through memory
                 codes = sv["pre_pool"][prev.idx]
-                if dispatch.current().poolbwd_fused:
+                if dispatch.current().poolbwd_fused and dispatch.current().tail_split and prev.idx == 1 and \
+                        dy.shape[0] >= 2:
+                    # the step's tail: conv1_2's weight gradient (~1 ms, the last kernel of the step) waited for
+                    # ALL of conv2_1's data gradient.  Image halves: conv1_2's weight gradient on the first half
+                    # runs (side stream) under the data gradient of the second half
+                    xp = sv["front_in"][prev.idx]
+                    n = dy.shape[0]
+                    full = torch.empty(n, 2 * dy.shape[1], 2 * dy.shape[2], prev.cout, dtype=dy.dtype,
+                                       device=dy.device)
+                    for k, (i0, i1) in enumerate(((0, n // 2), (n // 2, n))):
+                        if fuse_bias:
+                            _, bph = C.conv_dgrad_with_bias(dy[i0:i1], dgr, ksize=3, dil=1, epi=C.EPI_POOLBWD,
+                                                            mask=codes[i0:i1], out=full[i0:i1])
+                        else:
+                            C.conv_igemm(dy[i0:i1], dgr, None, ksize=3, dil=1, epi=C.EPI_POOLBWD,
+                                         mask=codes[i0:i1], out=full[i0:i1])
+                            bph = None
+                        wg(prev, full[i0:i1], xp[i0:i1], 3, 1, prev.first, prev.w_index, prev.b_index, bph,
+                           wbeta=None if k == 0 else 1.0, mark=k == 1)
+                    wg_done.add(prev.idx)
+                    dy, bp = full, None
+                elif dispatch.current().poolbwd_fused:
                     dy, bp = dgrad(dy, dgr, 1, C.EPI_POOLBWD, codes)
                 else:
                     dp = C.conv_igemm(dy, dgr, None, ksize=3, dil=1, epi=C.EPI_NONE)
