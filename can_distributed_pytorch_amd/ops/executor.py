@@ -419,11 +419,9 @@ class CANNetExecutor:
         dy = self._context_bwd(sv["ctx"], sv["fv"], dcat, grads, ws, beta, scale, ready, dscale, side, hold)
         # ---- frontend, reverse
         bp = None
-        wg_done = set()          # layers whose weight gradient already ran (image halves, tail_split)
         for s in reversed(self.front):
             x = sv["front_in"][s.idx]
-            if s.idx not in wg_done:
-                wg(s, dy, x, 3, 1, s.first, s.w_index, s.b_index, bp)
+            wg(s, dy, x, 3, 1, s.first, s.w_index, s.b_index, bp)
             if s.idx == 0:
                 break
             _, dgr = self.packs[id(s.module.weight)]
@@ -446,28 +444,9 @@ class CANNetExecutor:
                 # (+ ReLU mask of the pool input) in the conv epilogue: the pooled gradient never
                 # round-trips through memory
                 codes = sv["pre_pool"][prev.idx]
-                if dispatch.current().poolbwd_fused and dispatch.current().tail_split and prev.idx == 1 and \
-                        dy.shape[0] >= 2:
-                    # the step's tail: conv1_2's weight gradient (~1 ms, the last kernel of the step) waited for
-                    # ALL of conv2_1's data gradient.  Image halves: conv1_2's weight gradient on the first half
-                    # runs (side stream) under the data gradient of the second half
-                    xp = sv["front_in"][prev.idx]
-                    n = dy.shape[0]
-                    full = torch.empty(n, 2 * dy.shape[1], 2 * dy.shape[2], prev.cout, dtype=dy.dtype,
-                                       device=dy.device)
-                    for k, (i0, i1) in enumerate(((0, n // 2), (n // 2, n))):
-                        if fuse_bias:
-                            _, bph = C.conv_dgrad_with_bias(dy[i0:i1], dgr, ksize=3, dil=1, epi=C.EPI_POOLBWD,
-                                                            mask=codes[i0:i1], out=full[i0:i1])
-                        else:
-                            C.conv_igemm(dy[i0:i1], dgr, None, ksize=3, dil=1, epi=C.EPI_POOLBWD,
-                                         mask=codes[i0:i1], out=full[i0:i1])
-                            bph = None
-                        wg(prev, full[i0:i1], xp[i0:i1], 3, 1, prev.first, prev.w_index, prev.b_index, bph,
-                           wbeta=None if k == 0 else 1.0, mark=k == 1)
-                    wg_done.add(prev.idx)
-                    dy, bp = full, None
-                elif dispatch.current().poolbwd_fused:
+                # (conv2_1's data gradient / conv1_2's weight gradient in image halves measured -0.5 %:
+                # profiles/r4/ab_tail_split.txt)
+                if dispatch.current().poolbwd_fused:
                     dy, bp = dgrad(dy, dgr, 1, C.EPI_POOLBWD, codes)
                 else:
                     dp = C.conv_igemm(dy, dgr, None, ksize=3, dil=1, epi=C.EPI_NONE)

@@ -145,15 +145,17 @@ def test_conv_wgrad_v2_row_aligned(n, h, w, ci, co, dil, bias, dispatch_cfg):
     # Cout = 64: the 64-channel tile (4 waves, two blocks per CU, 2-stage DMA lead)
     (1, 6, 64, 64, 64, 1, torch.bfloat16), (2, 9, 120, 128, 64, 2, torch.bfloat16),
     (1, 5, 200, 64, 64, 1, torch.float16), (3, 16, 256, 64, 64, 1, torch.bfloat16)])
-@pytest.mark.parametrize("adb", [0, 1])
-def test_wgrad_tap_ring(n, h, w, ci, co, dil, dtype, adb, dispatch_cfg):
+@pytest.mark.parametrize("adb,w8", [(0, 0), (1, 0), (1, 1)])
+def test_wgrad_tap_ring(n, h, w, ci, co, dil, dtype, adb, w8, dispatch_cfg):
     """Tap-ring weight gradient (cfg 12: 128 output channels x 9 taps of a 64-channel input slice, input rows in an
     LDS ring walked down 64-column chains, one chain per row phase for dilation 2) == the fp32 reference: ragged
     widths (W % 64 != 0) and heights, single-row maps, slices spanning several chains, bias through the column-sum
     path."""
     from can_distributed_pytorch_amd.ops import _ext
     from can_distributed_pytorch_amd.ops import conv as C
-    dispatch_cfg(wgrad_tap=3, wgrad_tap_adb=adb)
+    if w8 and co != 64:
+        pytest.skip("8-wave form: the 64-channel tile only")
+    dispatch_cfg(wgrad_tap=3, wgrad_tap_adb=adb, wgrad_tap_w8=w8)
     assert _ext.require().wgrad_plan(n * h * w, ci, co, 3, 0, 1024, dil, w)[2] == 12
     torch.manual_seed(16)
     x = torch.randn(n, h, w, ci, device="cuda").to(dtype)

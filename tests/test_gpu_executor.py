@@ -237,28 +237,3 @@ def test_native_stepper_row_ring_matches_per_tap_kernel(mode, dispatch_cfg):
             assert torch.equal(pa, pb), name
 
 
-
-def test_native_stepper_tail_split_matches_default(dispatch_cfg):
-    """dispatch tail_split = 1: conv2_1's data gradient and conv1_2's weight gradient in image halves (the second
-    half's weight gradient accumulates, beta 1) train like the whole-batch schedule (same kernels; dW1_2 sums its
-    pixel slabs in a different grouping)."""
-    from can_distributed_pytorch_amd.engine.native import NativeStepper
-    _, nat_a = _models(14)
-    nat_b = copy.deepcopy(nat_a)
-    init = [(n, p.detach().clone()) for n, p in nat_a.named_parameters()]
-    x = torch.randn(4, 3, 96, 128, device="cuda")
-    gt = torch.rand(4, 1, 12, 16, device="cuda")
-    a = NativeStepper("cuda", lr=1e-7, graph=False, model=nat_a)
-    b = NativeStepper("cuda", lr=1e-7, graph=False, model=nat_b)
-    la, lb = [], []
-    for _ in range(3):
-        dispatch_cfg(tail_split=0)
-        la.append(float(a.step(x, gt)))
-        dispatch_cfg(tail_split=1)
-        lb.append(float(b.step(x, gt)))
-    torch.cuda.synchronize()
-    assert la[0] == lb[0]
-    for u, v in zip(la, lb):
-        assert abs(u - v) <= 1e-3 * abs(u), (la, lb)
-    for (name, p0), pa, pb in zip(init, nat_a.parameters(), nat_b.parameters()):
-        assert _rel(pb - p0, pa - p0) < 1e-2, name
