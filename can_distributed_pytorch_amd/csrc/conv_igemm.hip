@@ -353,6 +353,12 @@ __device__ __forceinline__ int tile_pix(const ConvArgs2& a, int pt, int r) {
   } else if constexpr (RT != 0 && EPI != EPI_POOLFWD) {
     const int tx = a.W >> 7, q = pt / tx, cb = pt - q * tx;
     return (RT * q + (r >> 7)) * a.W + cb * 128 + (r & 127);
+  } else if constexpr (RT != 0 && EPI == EPI_POOLFWD) {
+    // row ring, 2 x 128 tiles: fragment f = r / 16 holds columns 8f .. 8f + 7 of both rows, lanes 0-7 row 0 and
+    // 8-15 row 1 (the ds_read_b128 lane groups then see 8 distinct pixels per chunk: conflict-free)
+    const int ncb = a.W >> 7;
+    const int rp = pt / ncb, cb = pt - rp * ncb;
+    return (2 * rp + ((r & 15) >> 3)) * a.W + cb * 128 + (r >> 4) * 8 + (r & 7);
   } else if constexpr (EPI == EPI_POOLFWD) {
     const int ncb = a.W / (TP / 2);
     const int rp = pt / ncb, cb = pt - rp * ncb;    // rp = n * H/2 + pooled row
@@ -487,7 +493,9 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
     if constexpr (EPI == EPI_POOLFWD) {
       // lanes 4q .. 4q+3 hold the window (2 columns x 2 rows) of one pooled pixel: max of the stored
       // (rounded) values over quad_perm [1,0,3,2] then [2,3,0,1]; this lane's window position in ATen
-      // order is p = row * 2 + column = (fr & 1) * 2 + ((fr >> 1) & 1)
+      // order is p = row * 2 + column = (fr & 1) * 2 + ((fr >> 1) & 1).  Row ring (RT != 0): the window is
+      // lanes 2q, 2q + 1, 2q + 8, 2q + 9 (quad_perm [1,0,3,2] then row_ror 8), p = (fr >> 3) * 2 + (fr & 1)
+      constexpr int DPP2 = (RT != 0) ? 0x128 : 0x4E;
       float r[16], own[16];
       unpack8h<DT>(o0, r);
       unpack8h<DT>(o1, r + 8);
@@ -496,26 +504,26 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
         own[c] = r[c];
         float t = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(r[c]), 0xB1, 0xF, 0xF, false));
         r[c] = fmaxf(r[c], t);
-        t = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(r[c]), 0x4E, 0xF, 0xF, false));
+        t = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(r[c]), DPP2, 0xF, 0xF, false));
         r[c] = fmaxf(r[c], t);
       }
       uint32_t cw0 = 0u, cw1 = 0u;
       if (a.codes != nullptr) {
-        const int pbit = 1 << ((fr & 1) * 2 + ((fr >> 1) & 1));
+        const int pbit = (RT != 0) ? 1 << ((fr >> 3) * 2 + (fr & 1)) : 1 << ((fr & 1) * 2 + ((fr >> 1) & 1));
 #pragma unroll
         for (int c = 0; c < 16; ++c) {
           int b = (own[c] == r[c]) ? pbit : 0;
           b |= __builtin_amdgcn_mov_dpp(b, 0xB1, 0xF, 0xF, false);
-          b |= __builtin_amdgcn_mov_dpp(b, 0x4E, 0xF, 0xF, false);
+          b |= __builtin_amdgcn_mov_dpp(b, DPP2, 0xF, 0xF, false);
           const uint32_t nib = (r[c] > 0.f) ? (uint32_t)(b & -b) : 0u;    // first max, ReLU mask
           if (c < 8) cw0 |= nib << (4 * c); else cw1 |= nib << (4 * (c - 8));
         }
       }
-      if ((fr & 3) == 0) {
+      if ((fr & ((RT != 0) ? 9 : 3)) == 0) {
         const int ncb = a.W / (TP / 2);
         const int rp = pt / ncb, cb = pt - rp * ncb;
         const int pr = wp * 64 * PW + i * 16 + fr;
-        const int pc = cb * (TP / 4) + (pr >> 4) * 4 + ((pr & 15) >> 2);
+        const int pc = cb * (TP / 4) + (pr >> 4) * 4 + ((RT != 0) ? ((pr & 7) >> 1) : ((pr & 15) >> 2));
         const size_t pp = (size_t)rp * (a.W >> 1) + pc;
         bf16_t* yp = a.yp + pp * a.Cout + chb;
         *reinterpret_cast<uint4*>(yp) = pack8h<DT>(r);
@@ -1226,7 +1234,10 @@ __global__ void __launch_bounds__(512, 1) conv_rring_kernel(ConvArgs2 a) {
                 "row-ring configs: 256 x (2 x 128) with a 3- or 4-stage row lead (counted barrier waits need >= 3, 4 slots "
                 "allow <= 4); 64 x (4 x 128) with a 2-stage lead and a full drain");
   static_assert(D == 1 || D == 2, "dilation 1 or 2");
-  static_assert(EPI != EPI_POOLFWD && EPI != EPI_CTXF && EPI != EPI_CTXB, "row-ring epilogues");
+  static_assert(EPI != EPI_CTXF && EPI != EPI_CTXB, "row-ring epilogues");
+  // EPI_POOLFWD: 2-row tiles of an aligned map, dilation 1; every wave computes both rows of its columns
+  constexpr bool PL = (EPI == EPI_POOLFWD);
+  static_assert(!PL || (TR == 2 && !RG && D == 1), "fused max-pool: aligned 2-row tiles");
   constexpr int NW = 8, WC = TC / 64, WP = NW / WC;
   constexpr int TP = 128 * TR, PW = TP / (64 * WP);  // pixel fragments per wave / 4
   constexpr int WPR = WP / TR;                       // waves per tile row
@@ -1367,12 +1378,22 @@ __global__ void __launch_bounds__(512, 1) conv_rring_kernel(ConvArgs2 a) {
       af[j] = __builtin_bit_cast(frag8_t, As[row * 8 + swz(row, chunk)]);
     }
     const int c = st / 9, tap = st - 9 * c, kh = (tap * 11) >> 5, kw = tap - 3 * kh;
-    const int hp = 8 + cbw + fr + (kw - 1) * D;    // slot pixel of this lane's column in fragment 0
-    const unsigned char* base =
-        ring + ((c * NR + kh * D + rt) & (RING - 1)) * RR_SLOT + hp * 128 + ((chunk ^ (hp & 7)) << 4);
+    if constexpr (PL) {
+      // fragment i: columns 8 i .. 8 i + 7 of the wave's 32 PW, lanes 0-7 tile row 0, 8-15 row 1 (tile_pix)
+      const int hp = 8 + wp * 32 * PW + (fr & 7) + (kw - 1) * D;
+      const unsigned char* base =
+          ring + ((c * NR + kh * D + (fr >> 3)) & (RING - 1)) * RR_SLOT + hp * 128 + ((chunk ^ (hp & 7)) << 4);
 #pragma unroll
-    for (int i = 0; i < 4 * PW; ++i)
-      bfr[i] = __builtin_bit_cast(frag8_t, *reinterpret_cast<const uint4*>(base + i * 2048));
+      for (int i = 0; i < 4 * PW; ++i)
+        bfr[i] = __builtin_bit_cast(frag8_t, *reinterpret_cast<const uint4*>(base + i * 1024));
+    } else {
+      const int hp = 8 + cbw + fr + (kw - 1) * D;    // slot pixel of this lane's column in fragment 0
+      const unsigned char* base =
+          ring + ((c * NR + kh * D + rt) & (RING - 1)) * RR_SLOT + hp * 128 + ((chunk ^ (hp & 7)) << 4);
+#pragma unroll
+      for (int i = 0; i < 4 * PW; ++i)
+        bfr[i] = __builtin_bit_cast(frag8_t, *reinterpret_cast<const uint4*>(base + i * 2048));
+    }
   };
   auto mma = [&](const frag8_t (&af)[4], const frag8_t (&bfr)[4 * PW], int i0, int i1) {
 #pragma unroll
@@ -2099,93 +2120,114 @@ static bool use_ws64() { return g_dispatch.ws64 != 0; }
 // First layer (conv1_1: 3 -> 64, 3x3, input NHWC4 bf16 = 8 B per pixel).
 // Output-write bound (805 MB of bf16 activations at batch 8 x 768 x 1024), so
 // the kernel does the minimum around the stores: the 6 x 130-pixel input halo
-// of a 4 x 128 output tile goes to LDS once (6.2 KB, plain 8-B loads); the
+// of a 4 x 128 output tile goes to LDS (6.2 KB, plain 8-B loads); the
 // weights (packed [64][64], k = tap*4 + c) are MFMA A fragments loaded straight
 // into registers; each B fragment is two ds_read_b64 (taps 2q, 2q+1 of one
 // pixel, 4 channels each); K = 64 = 2 MFMA k-steps (taps 9..15 are zero).
+// Persistent (PF): two blocks per CU walk the tiles; a block loads the NEXT
+// tile's halo into registers before it computes and stores the current one and
+// parks it in the other LDS buffer afterwards, so its store stream never waits
+// on a halo load (one tile per block: 0.268 ms = 3.0 TB/s of stores).
+// Lane q of the D layout owns channels 8q .. 8q + 7 and 32 + 8q .. 32 + 8q + 7
+// (A row j*16 + 4q + r holds channel 32 (j >> 1) + 8q + 4 (j & 1) + r): each of a
+// wave's two 16-B stores covers 64 contiguous bytes of 16 pixels (16-B pieces
+// 32 B apart with perm_row: 0.268 -> 0.261 ms).
 // ===========================================================================
-template <int DT>
-__global__ void __launch_bounds__(512) conv_first_halo_kernel(HaloConvArgs a) {
+__device__ __forceinline__ int perm_row_st64(int rho) {
+  const int jt = rho >> 4, q = (rho >> 2) & 3, r = rho & 3;
+  return ((jt >> 1) << 5) | (q << 3) | ((jt & 1) << 2) | r;
+}
+template <int DT, bool PF>
+__global__ void __launch_bounds__(512, 4) conv_first_halo_kernel(HaloConvArgs a) {   // 2 blocks per CU: <= 128 VGPRs
   constexpr int TR = 4, TCOL = 128, HC = TCOL + 2, HPIX = (TR + 2) * HC;
-  __shared__ uint2 halo[HPIX];
+  static_assert(HPIX <= 1024, "two halo pixels per thread");
+  __shared__ uint2 halo[PF ? 2 : 1][HPIX];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntile = a.N * a.tiles_y * a.tiles_x;
-  const int tile = xcd_remap(blockIdx.x, ntile);
-  const int tx = tile % a.tiles_x;
-  const int ty = (tile / a.tiles_x) % a.tiles_y;
-  const int n = tile / (a.tiles_x * a.tiles_y);
-  const int oh0 = ty * TR, ow0 = tx * TCOL;
   const uint2* x8 = reinterpret_cast<const uint2*>(a.x);
-  for (int hp = tid; hp < HPIX; hp += 512) {
-    const int hr = hp / HC, hc = hp - hr * HC;
-    const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
-    uint2 v = make_uint2(0u, 0u);
-    if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) v = x8[(size_t)(n * a.H + ih) * a.W + iw];
-    halo[hp] = v;
-  }
+  // halo pixels tid and tid + 512 of tile t (zero outside the map / past HPIX)
+  auto load = [&](int t, uint2 (&v)[2]) {
+    const int tx = t % a.tiles_x, ty = (t / a.tiles_x) % a.tiles_y, n = t / (a.tiles_x * a.tiles_y);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int hp = tid + 512 * k;
+      const int hr = hp / HC, hc = hp - hr * HC;
+      const int ih = ty * TR - 1 + hr, iw = tx * TCOL - 1 + hc;
+      v[k] = make_uint2(0u, 0u);
+      if (hp < HPIX && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) v[k] = x8[(size_t)(n * a.H + ih) * a.W + iw];
+    }
+  };
+  auto park = [&](int b, const uint2 (&v)[2]) {
+    halo[b][tid] = v[0];
+    if (tid + 512 < HPIX) halo[b][tid + 512] = v[1];
+  };
   const int fr = lane & 15, fq = lane >> 4;
   frag8_t af[2][4];
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      af[kk][j] = __builtin_bit_cast(frag8_t, *reinterpret_cast<const uint4*>(a.w + perm_row(j * 16 + fr) * 64 + kk * 32 + fq * 8));
-  __syncthreads();
-
-  const int r = wave >> 1, colbase = (wave & 1) * 64;
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    const int t0 = kk * 8 + fq * 2;                 // this lane's taps t0, t0+1
-    frag8_t bfr[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      uint2 lo = make_uint2(0u, 0u), hi = make_uint2(0u, 0u);
-      const int c = colbase + i * 16 + fr;
-      if (t0 < 9) {
-        const int kh = (t0 * 11) >> 5, kw = t0 - kh * 3;
-        lo = halo[(r + kh) * HC + c + kw];
-      }
-      if (t0 + 1 < 9) {
-        const int kh = ((t0 + 1) * 11) >> 5, kw = t0 + 1 - kh * 3;
-        hi = halo[(r + kh) * HC + c + kw];
-      }
-      bfr[i] = __builtin_bit_cast(frag8_t, make_uint4(lo.x, lo.y, hi.x, hi.y));
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        acc[j][i] = mfma16<DT>(af[kk][j], bfr[i], acc[j][i]);
-  }
-
-  const int oh = oh0 + r;
-  if (oh >= a.H) return;
-  const int chb = fq * 16;
+      af[kk][j] = __builtin_bit_cast(frag8_t, *reinterpret_cast<const uint4*>(a.w + perm_row_st64(j * 16 + fr) * 64 + kk * 32 + fq * 8));
+  const int chb = fq * 8;                              // channel of v[0]; v[8] at chb + 32
   float bias[16];
 #pragma unroll
   for (int c = 0; c < 16; c += 4) {
-    const float4 b4 = *reinterpret_cast<const float4*>(a.bias + chb + c);
+    const float4 b4 = *reinterpret_cast<const float4*>(a.bias + chb + (c < 8 ? c : 24 + c));
     bias[c] = b4.x; bias[c + 1] = b4.y; bias[c + 2] = b4.z; bias[c + 3] = b4.w;
   }
+  const int r = wave >> 1, colbase = (wave & 1) * 64;
+
+  int t = PF ? (int)blockIdx.x : xcd_remap(blockIdx.x, ntile);
+  const int tstep = PF ? (int)gridDim.x : ntile;
+  uint2 nv[2];
+  load(t, nv);
+  park(0, nv);
+  __syncthreads();
+  for (int it = 0; t < ntile; ++it, t += tstep) {
+    const int b = PF ? (it & 1) : 0;
+    const bool more = PF && t + tstep < ntile;
+    if (more) load(t + tstep, nv);                   // in flight under this tile's MFMAs and stores
+    const int tx = t % a.tiles_x, ty = (t / a.tiles_x) % a.tiles_y, n = t / (a.tiles_x * a.tiles_y);
+    const int oh = ty * TR + r;
+    // one 16-pixel fragment at a time (16 accumulator registers live, not 64: two blocks per CU fit)
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int ow = ow0 + colbase + i * 16 + fr;
-    if (ow >= a.W) continue;
-    float v[16];
+    for (int i = 0; i < 4; ++i) {
+      f32x4 acc[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int c = colbase + i * 16 + fr;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[j * 4 + q] = fmaxf(acc[j][i][q] + bias[j * 4 + q], 0.f);
-    const size_t off = ((size_t)(n * a.H + oh) * a.W + ow) * 64 + chb;
-    *reinterpret_cast<uint4*>(a.y + off) =
-        make_uint4(pack2<DT>(v[0], v[1]), pack2<DT>(v[2], v[3]), pack2<DT>(v[4], v[5]), pack2<DT>(v[6], v[7]));
-    *reinterpret_cast<uint4*>(a.y + off + 8) =
-        make_uint4(pack2<DT>(v[8], v[9]), pack2<DT>(v[10], v[11]), pack2<DT>(v[12], v[13]), pack2<DT>(v[14], v[15]));
+      for (int kk = 0; kk < 2; ++kk) {
+        const int t0 = kk * 8 + fq * 2;               // this lane's taps t0, t0+1
+        uint2 lo = make_uint2(0u, 0u), hi = make_uint2(0u, 0u);
+        if (t0 < 9) {
+          const int kh = (t0 * 11) >> 5, kw = t0 - kh * 3;
+          lo = halo[b][(r + kh) * HC + c + kw];
+        }
+        if (t0 + 1 < 9) {
+          const int kh = ((t0 + 1) * 11) >> 5, kw = t0 + 1 - kh * 3;
+          hi = halo[b][(r + kh) * HC + c + kw];
+        }
+        const frag8_t bfr = __builtin_bit_cast(frag8_t, make_uint4(lo.x, lo.y, hi.x, hi.y));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = mfma16<DT>(af[kk][j], bfr, acc[j]);
+      }
+      const int ow = tx * TCOL + c;
+      if (oh >= a.H || ow >= a.W) continue;
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[j * 4 + q] = fmaxf(acc[j][q] + bias[j * 4 + q], 0.f);
+      const size_t off = ((size_t)(n * a.H + oh) * a.W + ow) * 64 + chb;
+      *reinterpret_cast<uint4*>(a.y + off) =
+          make_uint4(pack2<DT>(v[0], v[1]), pack2<DT>(v[2], v[3]), pack2<DT>(v[4], v[5]), pack2<DT>(v[6], v[7]));
+      *reinterpret_cast<uint4*>(a.y + off + 32) =
+          make_uint4(pack2<DT>(v[8], v[9]), pack2<DT>(v[10], v[11]), pack2<DT>(v[12], v[13]), pack2<DT>(v[14], v[15]));
+    }
+    if (!PF) break;
+    if (more) park(b ^ 1, nv);                       // buffer b ^ 1 was last read two tiles ago (barrier since)
+    __syncthreads();
   }
 }
 
@@ -2300,7 +2342,18 @@ static int conv_igemm_impl(const void* x, const void* w, const float* bias, cons
       HaloConvArgs h;
       h.x = a.x; h.w = a.w; h.bias = a.bias; h.mask = nullptr; h.y = a.y; h.zero = nullptr;
       h.N = N; h.H = H; h.W = W; h.tiles_x = (W + 127) / 128; h.tiles_y = (H + 3) / 4;
-      hipLaunchKernelGGL(conv_first_halo_kernel<DT>, dim3(N * h.tiles_y * h.tiles_x), dim3(512), 0, s, h);
+      const int ntile = N * h.tiles_y * h.tiles_x;
+      if (g_dispatch.first_pf) {
+        static int ncu = 0;
+        if (!ncu) {
+          int dev = 0;
+          CAN_HIP_CHECK(hipGetDevice(&dev));
+          CAN_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+        }
+        hipLaunchKernelGGL((conv_first_halo_kernel<DT, true>), dim3(std::min(ntile, 2 * ncu)), dim3(512), 0, s, h);
+      } else {
+        hipLaunchKernelGGL((conv_first_halo_kernel<DT, false>), dim3(ntile), dim3(512), 0, s, h);
+      }
       return (int)hipGetLastError();
     }
     CAN_EPI_CASE(LOAD_FIRST, EPI_BIAS_RELU)
@@ -2434,6 +2487,22 @@ static int conv_pool_fwd_impl(const void* x, const void* w, const float* bias, v
                               int N, int H, int W, int Cin, int Cout, int ksize, int dil, int tile_cfg,
                               hipStream_t s) {
   if (Cout % 64 || Cin % 64 || H < 2 || W < 2) return -3;
+  if (ksize == 3 && dil == 1 && H % 2 == 0 && W % 128 == 0 && Cin % 64 == 0 &&
+      ((tile_cfg == 0 && g_dispatch.rring_pool && Cout % 256 == 0) || (tile_cfg == 27 && Cout % 256 == 0) ||
+       (tile_cfg == 29 && Cout % 128 == 0))) {
+    // row ring with the max-pool in the epilogue: 256 x (2 x 128) tiles (Cout % 256 == 0) or 128 x (2 x 128).
+    // Default (dispatch rring_pool) only the 256-channel form: conv3_3 + pool 0.429 -> 0.384 ms; the 128-channel
+    // one loses to conv_glds2's 128 x 512 tile on conv2_2 (0.588 -> 0.639 ms), profiles/r4/ab_rring_pool.txt
+    ConvArgs2 b;
+    b.x = (const bf16_t*)x; b.w = (const bf16_t*)w; b.bias = bias; b.mask = nullptr; b.y = (bf16_t*)y;
+    b.yp = (bf16_t*)yp; b.codes = (uint32_t*)codes; b.zero = conv_zero_page();
+    if (!b.zero) return -10;
+    b.H = H; b.W = W; b.Cin = Cin; b.Cout = Cout; b.ksize = ksize; b.dil = dil; b.M = N * H * W;
+    b.fdW = make_fastdiv((uint32_t)W); b.fdH = make_fastdiv((uint32_t)H);
+    const bool wide = (tile_cfg == 27) || (tile_cfg == 0 && Cout % 256 == 0);
+    return wide ? launch_rring_rg<DT, EPI_POOLFWD, 256, 2, 3, 1, false>(b, s)
+                : launch_rring_rg<DT, EPI_POOLFWD, 128, 2, 3, 1, false>(b, s);
+  }
   if (Cin == 64 && Cout == 64 && ksize == 3 && dil == 1 && tile_cfg == 0) {
     // conv1_2: halo-tiled kernel, 4 x 64 output tiles (full tiles only: the pool epilogue has barriers)
     if (H % 4 || W % 64) return -13;
@@ -2529,5 +2598,7 @@ extern "C" int can_conv_plan(int H, int W, int Cin, int Cout, int ksize, int dil
 // needs H even and W % (tp / 2) == 0
 extern "C" int can_conv_pool_tp(int Cin, int Cout, int ksize, int tile_cfg) {
   if (Cin == 64 && Cout == 64 && ksize == 3 && tile_cfg == 0) return 128;   // halo kernel: W % 64 (and H % 4)
+  // row ring (2 x 128 tiles, 3x3 only): explicit cfg 27 (Cout % 256) / 29 (Cout % 128)
+  if (tile_cfg == 27 || tile_cfg == 29) return (ksize == 3 && Cout % (tile_cfg == 27 ? 256 : 128) == 0) ? 256 : 0;
   return can::glds_cfg_tp(tile_cfg ? tile_cfg : can::glds_default_cfg(Cin, Cout, ksize));
 }

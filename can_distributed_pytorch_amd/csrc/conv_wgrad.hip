@@ -1312,7 +1312,7 @@ extern "C" int can_wgrad_plan(int M, int Cin, int Cout, int ksize, int first, in
     // one block per CU (TCO 128) or two (TCO 64)
     const int ntile = (Cin / 64) * (Cout / tco);
     const int stages = (M / W) * ((W + 63) / 64);
-    const int slots_per_cu = (tco == 128 || g_dispatch.wgrad_tap_w8) ? 1 : 2;
+    const int slots_per_cu = (tco == 128) ? 1 : 2;
     int S = 0;
     for (int R = 1; R <= 8 && !S; ++R) {
       const int s = (ncu * slots_per_cu * R) / ntile;
@@ -1443,9 +1443,6 @@ static int conv_wgrad_impl(const void* dy, const void* x, float* ws, float* wsb,
       if (wgrad_tap_tco(Cout) == 128) {
         if (adb) rc = (dil == 1) ? launch_wgrad_tap<DT, 1, 128, true>(t, s) : launch_wgrad_tap<DT, 2, 128, true>(t, s);
         else rc = (dil == 1) ? launch_wgrad_tap<DT, 1, 128, false>(t, s) : launch_wgrad_tap<DT, 2, 128, false>(t, s);
-      } else if (g_dispatch.wgrad_tap_w8) {
-        if (adb) rc = (dil == 1) ? launch_wgrad_tap<DT, 1, 64, true, true>(t, s) : launch_wgrad_tap<DT, 2, 64, true, true>(t, s);
-        else rc = (dil == 1) ? launch_wgrad_tap<DT, 1, 64, false, true>(t, s) : launch_wgrad_tap<DT, 2, 64, false, true>(t, s);
       } else {
         if (adb) rc = (dil == 1) ? launch_wgrad_tap<DT, 1, 64, true>(t, s) : launch_wgrad_tap<DT, 2, 64, true>(t, s);
         else rc = (dil == 1) ? launch_wgrad_tap<DT, 1, 64, false>(t, s) : launch_wgrad_tap<DT, 2, 64, false>(t, s);

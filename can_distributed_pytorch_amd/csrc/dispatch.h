@@ -24,7 +24,8 @@ struct DispatchConfig {
   // ones, 3 + the Cout = 64 layers (64-channel tile, two blocks per CU): step 495.6 -> 511.8 (1) / 516.5 (2) img/s, 3 interleaved rounds (profiles/r4/ab_wgrad_tap.txt)
   int wgrad_tap = 3;        // 3: 521.4 vs 518.4 img/s (2), 3 interleaved rounds (profiles/r4/ab_wgrad_tap_variants.txt)
   int wgrad_tap_adb = 1;    // tap ring: double-buffered dY fragments (step +0.45 %, same file)
-  int wgrad_tap_w8 = 0;     // tap ring, Cout = 64: 8 waves of 32 channels, one block per CU (A/B)
+  int first_pf = 1;        // conv1_1: persistent, next halo loaded under the current stores (0.272 -> 0.189 ms)
+  int rring_pool = 1;       // conv + 2x2 max-pool on the row ring (Cout % 256: conv3_3 -10 %, step +0.2 %)
 };
 
 // the process-wide configuration (defined in bindings.cpp)

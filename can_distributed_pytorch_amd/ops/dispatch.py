@@ -34,7 +34,8 @@ class DispatchConfig:
     wgrad_tap: int = 3        # tap-ring weight gradient (cfg 12): 0 off, 1 v2-GEMM layers, 2 + Cout-128 ring layers,
     #                           3 + Cout-64 layers
     wgrad_tap_adb: int = 1    # tap ring: double-buffered dY fragments
-    wgrad_tap_w8: int = 0     # tap ring, Cout = 64: 8 waves of 32 channels, one block per CU
+    first_pf: int = 1        # conv1_1: persistent, next tile's halo loaded under the current stores
+    rring_pool: int = 1       # conv + 2x2 max-pool on the row ring (Cout % 256 layers)
     # ---- executor / front-end (Python)
     w1g: int = 1              # conv1_1's weight gradient fused into conv1_2's data gradient
     pool_fwd_fused: int = 1   # 2x2 max-pool in the conv epilogue
@@ -46,7 +47,7 @@ class DispatchConfig:
     ctx_wgrad_cus: int = 224  # CUs the batched context 1x1 weight gradient is planned for
 
     NATIVE = ("rring", "rring64", "rring128", "ws64", "ctx_tile_f", "ctx_tile_b", "wgrad_halo_ring", "ring_fast",
-              "ring_skew", "reduce_tiled", "wgrad_tap", "wgrad_tap_adb", "wgrad_tap_w8")
+              "ring_skew", "reduce_tiled", "wgrad_tap", "wgrad_tap_adb", "rring_pool", "first_pf")
 
     def native(self) -> Dict[str, int]:
         return {k: getattr(self, k) for k in self.NATIVE}
@@ -55,7 +56,7 @@ class DispatchConfig:
 _ALLOWED = {
     "rring": (0, 1, 2), "rring64": (0, 1), "rring128": (0, 1, 2, 3), "ws64": (0, 1), "ctx_tile_f": (128, 256),
     "ctx_tile_b": (128, 256), "wgrad_halo_ring": (0, 1), "ring_fast": (0, 1), "ring_skew": (0, 1),
-    "reduce_tiled": (0, 1), "wgrad_tap": (0, 1, 2, 3), "wgrad_tap_adb": (0, 1), "wgrad_tap_w8": (0, 1), "w1g": (0, 1), "pool_fwd_fused": (0, 1), "poolbwd_fused": (0, 1), "ctx_linear": (0, 1),
+    "reduce_tiled": (0, 1), "wgrad_tap": (0, 1, 2, 3), "wgrad_tap_adb": (0, 1), "rring_pool": (0, 1), "first_pf": (0, 1), "w1g": (0, 1), "pool_fwd_fused": (0, 1), "poolbwd_fused": (0, 1), "ctx_linear": (0, 1),
     "ctx_batched": (0, 1), "bias_fused": (0, 1), "wgrad_stream": (0, 1),
 }
 

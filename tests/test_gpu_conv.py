@@ -51,10 +51,12 @@ def test_conv_fwd(n, h, w, ci, co, k, dil, tile):
     _close(y, _ref(x, wt, b, dil))
 
 
+@pytest.mark.parametrize("pf", [0, 1])
 @pytest.mark.parametrize("n,h,w,tile", [(2, 40, 56, 0), (1, 37, 150, 0), (2, 8, 256, 0), (2, 40, 56, 32)])
-def test_conv_first_layer(n, h, w, tile):
-    """tile 0 (auto) / 32: halo-tiled first-layer kernel."""
+def test_conv_first_layer(n, h, w, tile, pf, dispatch_cfg):
+    """tile 0 (auto) / 32: halo-tiled first-layer kernel (pf: persistent, prefetching the next tile's halo)."""
     from can_distributed_pytorch_amd.ops import conv as C
+    dispatch_cfg(first_pf=pf)
     torch.manual_seed(1)
     img = torch.randn(n, 3, h, w, device="cuda")
     wt = (torch.randn(64, 3, 3, 3, device="cuda") * 0.2).to(torch.bfloat16).float()
@@ -145,17 +147,15 @@ def test_conv_wgrad_v2_row_aligned(n, h, w, ci, co, dil, bias, dispatch_cfg):
     # Cout = 64: the 64-channel tile (4 waves, two blocks per CU, 2-stage DMA lead)
     (1, 6, 64, 64, 64, 1, torch.bfloat16), (2, 9, 120, 128, 64, 2, torch.bfloat16),
     (1, 5, 200, 64, 64, 1, torch.float16), (3, 16, 256, 64, 64, 1, torch.bfloat16)])
-@pytest.mark.parametrize("adb,w8", [(0, 0), (1, 0), (1, 1)])
-def test_wgrad_tap_ring(n, h, w, ci, co, dil, dtype, adb, w8, dispatch_cfg):
+@pytest.mark.parametrize("adb", [0, 1])
+def test_wgrad_tap_ring(n, h, w, ci, co, dil, dtype, adb, dispatch_cfg):
     """Tap-ring weight gradient (cfg 12: 128 output channels x 9 taps of a 64-channel input slice, input rows in an
     LDS ring walked down 64-column chains, one chain per row phase for dilation 2) == the fp32 reference: ragged
     widths (W % 64 != 0) and heights, single-row maps, slices spanning several chains, bias through the column-sum
     path."""
     from can_distributed_pytorch_amd.ops import _ext
     from can_distributed_pytorch_amd.ops import conv as C
-    if w8 and co != 64:
-        pytest.skip("8-wave form: the 64-channel tile only")
-    dispatch_cfg(wgrad_tap=3, wgrad_tap_adb=adb, wgrad_tap_w8=w8)
+    dispatch_cfg(wgrad_tap=3, wgrad_tap_adb=adb)
     assert _ext.require().wgrad_plan(n * h * w, ci, co, 3, 0, 1024, dil, w)[2] == 12
     torch.manual_seed(16)
     x = torch.randn(n, h, w, ci, device="cuda").to(dtype)
@@ -320,6 +320,32 @@ def test_conv_pool_fwd_fused(n, h, w, ci, co, dil, dtype):
     if ci == 64 and co == 64:                                            # halo kernel: whole 4-row tiles
         assert not C.conv_pool_fwd_ok(x[:, :h - 2].contiguous(), co, 3)
         assert not C.conv_pool_fwd_ok(x[:, :, :w - 32].contiguous(), co, 3)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("n,h,w,ci,co,tile", [(2, 8, 256, 128, 128, 29), (1, 6, 128, 256, 256, 27),
+                                              (2, 4, 384, 64, 128, 29), (1, 10, 256, 128, 256, 0),
+                                              (2, 6, 256, 128, 128, 0)])
+def test_conv_pool_fwd_rring(n, h, w, ci, co, tile, dtype, dispatch_cfg):
+    """Row-ring conv with the max-pool in the epilogue (2-row tiles, both rows per wave; tile 0 = dispatch
+    rring_pool) == conv_igemm(EPI_BIAS_RELU) + max-pool codes, bitwise, with and without the full-size store."""
+    from can_distributed_pytorch_amd.ops import conv as C
+    dispatch_cfg(rring_pool=1)
+    torch.manual_seed(13)
+    x = torch.randn(n, h, w, ci, device="cuda").to(dtype)
+    wt = torch.randn(co, ci, 3, 3, device="cuda") * (2.0 / (9 * ci)) ** 0.5
+    b = torch.randn(co, device="cuda") * 0.1
+    wp = C.pack_weight_fwd(wt, dtype)
+    assert C.conv_pool_fwd_ok(x, co, 3, tile)
+    y, yp, codes = C.conv_pool_fwd(x, wp, b, ksize=3, tile=tile, codes=True)
+    _, yp2, codes2 = C.conv_pool_fwd(x, wp, b, ksize=3, tile=tile, keep_full=False, codes=True)
+    y_ref = C.conv_igemm(x, wp, b, ksize=3)
+    yp_ref, codes_ref = C.maxpool_codes(y_ref)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_ref)
+    assert torch.equal(yp, yp_ref) and torch.equal(codes, codes_ref)
+    assert torch.equal(yp2, yp) and torch.equal(codes2, codes)
+    assert torch.equal(yp_ref, F.max_pool2d(y_ref.permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1))
 
 
 @pytest.mark.parametrize("n,h,w,ci,co,dil,beta", [(2, 8, 64, 512, 256, 2, 0.0), (1, 6, 128, 1024, 512, 1, 1.0),
