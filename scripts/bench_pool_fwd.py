@@ -28,7 +28,7 @@ def main():
         wp = C.pack_weight_fwd(torch.randn(co, ci, 3, 3, device="cuda") * (2.0 / (9 * ci)) ** 0.5)
         b = torch.randn(co, device="cuda") * 0.1
         flops = 2.0 * args.batch * h * w * ci * co * 9
-        tiles = [0] + ([29] if co % 128 == 0 else []) + ([27] if co % 256 == 0 else [])
+        tiles = [0] + ([29, 22, 25] if co % 128 == 0 and ci > 64 else []) + ([27] if co % 256 == 0 else [])
         ref = None
         for tile in tiles:
             with dispatch.override(rring_pool=0):
@@ -51,6 +51,19 @@ def main():
                    "bitwise_vs_tile0": same}
             out.append(rec)
             print(json.dumps(rec), flush=True)
+        # the same conv without the pool (full-resolution store), default kernel
+        fn = lambda: C.conv_igemm(x, wp, b, ksize=3)
+        for _ in range(3):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(args.iters):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / args.iters
+        print(json.dumps({"layer": name, "plain_conv_ms": round(ms, 4)}), flush=True)
 
 
 if __name__ == "__main__":
