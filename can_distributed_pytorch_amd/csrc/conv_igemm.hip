@@ -1796,6 +1796,15 @@ conv_halo64_kernel(HaloConvArgs a) {
 // earlier (a counted wait would be unsafe: loads and stores retire out of
 // order with respect to each other).
 // ===========================================================================
+// W1G staging of the produced dY tile: tile pixel px (row * 64 + column) = 128-B row of 16 8-byte units (4 channels
+// each), unit c8 at c8 ^ (((px >> 1) & 1 | ((px >> 3) & 1) << 1) << 2): the conv1_1 weight-gradient phase reads its
+// A fragments (16 channels x 32 pixels, pixel-contiguous per lane) with two ds_read_b64_tr_b16 each
+typedef short w1g_s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) w1g_s16x4 w1g_lds_s16x4;
+__device__ __forceinline__ unsigned w1g_off(int px, int c8) {
+  return (unsigned)(px * 128 + ((c8 ^ ((((px >> 1) & 1) | (((px >> 3) & 1) << 1)) << 2)) * 8));
+}
+
 template <int DT, int EPI, bool W1G = false>
 __global__ void __launch_bounds__(512, 1) conv_ws64_kernel(HaloConvArgs a) {
   // halo rows of 66 pixels stored at a 72-pixel stride: a 1-KiB DMA piece (8 pixels) never straddles two
@@ -1981,9 +1990,15 @@ __global__ void __launch_bounds__(512, 1) conv_ws64_kernel(HaloConvArgs a) {
       const uint4 o = pack8h<DT>(v);
       if (row_ok && ow < a.W && ((EPI != EPI_POOLFWD && !W1G) || a.y != nullptr))
         *reinterpret_cast<uint4*>(a.y + ((size_t)(n * a.H + oh) * a.W + ow) * 64 + chb) = o;
-      if constexpr (EPI == EPI_POOLFWD || W1G) {
+      if constexpr (EPI == EPI_POOLFWD) {
         // staging tile [4 rows][64 cols] x 128 B in `cur`, 16-B chunk c of column col at slot c ^ (col & 7)
         reinterpret_cast<uint4*>(cur + (r * 64 + col) * 128)[(h * 4 + fq) ^ (col & 7)] = o;
+      }
+      if constexpr (W1G) {
+        // staging tile in `cur` (w1g_off layout): channels chb .. chb + 7 = units 8h + 2fq, 8h + 2fq + 1
+        const int px = r * 64 + col, c8 = h * 8 + fq * 2;
+        *reinterpret_cast<uint2*>(cur + w1g_off(px, c8)) = make_uint2(o.x, o.y);
+        *reinterpret_cast<uint2*>(cur + w1g_off(px, c8 + 1)) = make_uint2(o.z, o.w);
       }
     }
     if constexpr (EPI == EPI_POOLFWD) {
@@ -2036,24 +2051,22 @@ __global__ void __launch_bounds__(512, 1) conv_ws64_kernel(HaloConvArgs a) {
       int ln = lane;
       asm volatile("" : "+v"(ln));                   // lane math stays in this phase (not hoisted out of the loop)
       const int fr = ln & 15, fq = ln >> 4;
-      const int co = cb * 16 + fr;
+      const int qd = (ln & 15) >> 2, p4 = ln & 3;
       f32x4 wacc[3];
 #pragma unroll
       for (int nb = 0; nb < 3; ++nb) wacc[nb] = waccl[nb * 64];
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) {
         const int row = 2 * ph + (s4 >> 1), colb = (s4 & 1) * 32 + fq * 8;
-        unsigned av[4];
-#pragma unroll
-        for (int e = 0; e < 8; e += 2) {
-          const int c0 = colb + e, c1 = colb + e + 1;
-          const unsigned short u0 = *reinterpret_cast<const unsigned short*>(
-              cur + (row * 64 + c0) * 128 + (((co >> 3) ^ (c0 & 7)) * 16) + (co & 7) * 2);
-          const unsigned short u1 = *reinterpret_cast<const unsigned short*>(
-              cur + (row * 64 + c1) * 128 + (((co >> 3) ^ (c1 & 7)) * 16) + (co & 7) * 2);
-          av[e >> 1] = (unsigned)u0 | ((unsigned)u1 << 16);
-        }
-        const frag8_t afr = __builtin_bit_cast(frag8_t, make_uint4(av[0], av[1], av[2], av[3]));
+        // A = dY^T (channels cb*16 + fr, pixels colb .. colb + 7 of this lane's k group): lo = pixels + 0..3,
+        // hi = + 4..7 (transposed 8-byte reads of units 4cb + p4 of pixel rows 8fq + qd, 8fq + qd + 4)
+        const int px0 = row * 64 + (s4 & 1) * 32 + 8 * fq + qd;
+        const w1g_s16x4 alo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((w1g_lds_s16x4*)(cur + w1g_off(px0, 4 * cb + p4)));
+        const w1g_s16x4 ahi =
+            __builtin_amdgcn_ds_read_tr16_b64_v4i16((w1g_lds_s16x4*)(cur + w1g_off(px0 + 4, 4 * cb + p4)));
+        typedef short s16x8_t __attribute__((ext_vector_type(8)));
+        const s16x8_t a8 = {alo[0], alo[1], alo[2], alo[3], ahi[0], ahi[1], ahi[2], ahi[3]};
+        const frag8_t afr = __builtin_bit_cast(frag8_t, a8);
 #pragma unroll
         for (int nb = 0; nb < 3; ++nb) {
           const int nn = nb * 16 + fr;
