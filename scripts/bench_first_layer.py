@@ -32,7 +32,7 @@ def main(iters=20):
                 e1.record()
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / iters
-            print(json.dumps({"round": rnd, "first_pf": st, "ms": round(ms, 4),
+            print(json.dumps({"round": rnd, "arm": ["one tile per block", "persistent + LDS-staged stores"][st], "ms": round(ms, 4),
                               "write_TBps": round(y.numel() * 2 / ms / 1e9, 2), "bitwise": same}), flush=True)
 
 
