@@ -368,6 +368,34 @@ __device__ __forceinline__ int tile_pix(const ConvArgs2& a, int pt, int r) {
   }
 }
 
+// two 16-bit lanes per VGPR (the max-pool epilogue works on the stored bf16 / fp16 bit patterns: after the ReLU they
+// are non-negative, where the unsigned order of the bits is the order of the values)
+__device__ __forceinline__ unsigned pk_max_u16(unsigned a, unsigned b) {
+  unsigned r;
+  asm("v_pk_max_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ unsigned pk_min_u16(unsigned a, unsigned b) {
+  unsigned r;
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ unsigned pk_sub_u16(unsigned a, unsigned b) {
+  unsigned r;
+  asm("v_pk_sub_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ unsigned pk_lshl_b16(unsigned v, unsigned sh) {
+  unsigned r;
+  asm("v_pk_lshlrev_b16 %0, %1, %2" : "=v"(r) : "v"(sh), "v"(v));
+  return r;
+}
+__device__ __forceinline__ unsigned pk_mul_lo_u16(unsigned a, unsigned b) {
+  unsigned r;
+  asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 // Shared epilogue of the LDS-DMA kernels: lane (fr, fq) of wave (wc, wp) owns
 // 16 consecutive output channels of one pixel per 16x16 pixel fragment.
 template <int DT, int WC, int WP, int PW, int EPI, int RT = 0, bool RG = false>
@@ -496,27 +524,30 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
       // order is p = row * 2 + column = (fr & 1) * 2 + ((fr >> 1) & 1).  Row ring (RT != 0): the window is
       // lanes 2q, 2q + 1, 2q + 8, 2q + 9 (quad_perm [1,0,3,2] then row_ror 8), p = (fr >> 3) * 2 + (fr & 1)
       constexpr int DPP2 = (RT != 0) ? 0x128 : 0x4E;
-      float r[16], own[16];
-      unpack8h<DT>(o0, r);
-      unpack8h<DT>(o1, r + 8);
+      // on the stored 16-bit patterns, two channels per VGPR (channel 2k low half, 2k + 1 high half of word k);
+      // the sign bits are cleared so a -0 from the ReLU counts as +0
+      const unsigned ow[8] = {o0.x & 0x7FFF7FFFu, o0.y & 0x7FFF7FFFu, o0.z & 0x7FFF7FFFu, o0.w & 0x7FFF7FFFu,
+                              o1.x & 0x7FFF7FFFu, o1.y & 0x7FFF7FFFu, o1.z & 0x7FFF7FFFu, o1.w & 0x7FFF7FFFu};
+      unsigned mx[8];
 #pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        own[c] = r[c];
-        float t = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(r[c]), 0xB1, 0xF, 0xF, false));
-        r[c] = fmaxf(r[c], t);
-        t = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(r[c]), DPP2, 0xF, 0xF, false));
-        r[c] = fmaxf(r[c], t);
+      for (int k = 0; k < 8; ++k) {
+        mx[k] = pk_max_u16(ow[k], (unsigned)__builtin_amdgcn_mov_dpp((int)ow[k], 0xB1, 0xF, 0xF, false));
+        mx[k] = pk_max_u16(mx[k], (unsigned)__builtin_amdgcn_mov_dpp((int)mx[k], DPP2, 0xF, 0xF, false));
       }
       uint32_t cw0 = 0u, cw1 = 0u;
       if (a.codes != nullptr) {
-        const int pbit = (RT != 0) ? 1 << ((fr >> 3) * 2 + (fr & 1)) : 1 << ((fr & 1) * 2 + ((fr >> 1) & 1));
+        const unsigned ps = (RT != 0) ? (unsigned)((fr >> 3) * 2 + (fr & 1)) : (unsigned)((fr & 1) * 2 + ((fr >> 1) & 1));
+        const unsigned ps2 = ps | (ps << 16), one2 = 0x00010001u;
 #pragma unroll
-        for (int c = 0; c < 16; ++c) {
-          int b = (own[c] == r[c]) ? pbit : 0;
-          b |= __builtin_amdgcn_mov_dpp(b, 0xB1, 0xF, 0xF, false);
-          b |= __builtin_amdgcn_mov_dpp(b, DPP2, 0xF, 0xF, false);
-          const uint32_t nib = (r[c] > 0.f) ? (uint32_t)(b & -b) : 0u;    // first max, ReLU mask
-          if (c < 8) cw0 |= nib << (4 * c); else cw1 |= nib << (4 * (c - 8));
+        for (int k = 0; k < 8; ++k) {
+          // bit p of each half where this lane (window position p) holds the max, OR-ed over the window, the
+          // lowest set bit kept (first max), zeroed where the max is not > 0 (ReLU mask)
+          unsigned b = pk_lshl_b16(pk_sub_u16(one2, pk_min_u16(ow[k] ^ mx[k], one2)), ps2);
+          b |= (unsigned)__builtin_amdgcn_mov_dpp((int)b, 0xB1, 0xF, 0xF, false);
+          b |= (unsigned)__builtin_amdgcn_mov_dpp((int)b, DPP2, 0xF, 0xF, false);
+          const unsigned nib = pk_mul_lo_u16(b & pk_sub_u16(0u, b), pk_min_u16(mx[k], one2));
+          const unsigned byte = (nib & 0xFu) | ((nib >> 12) & 0xF0u);
+          if (k < 4) cw0 |= byte << (8 * k); else cw1 |= byte << (8 * (k - 4));
         }
       }
       if ((fr & ((RT != 0) ? 9 : 3)) == 0) {
@@ -526,8 +557,8 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs2& a, f32x4 (&acc)[4
         const int pc = cb * (TP / 4) + (pr >> 4) * 4 + ((RT != 0) ? ((pr & 7) >> 1) : ((pr & 15) >> 2));
         const size_t pp = (size_t)rp * (a.W >> 1) + pc;
         bf16_t* yp = a.yp + pp * a.Cout + chb;
-        *reinterpret_cast<uint4*>(yp) = pack8h<DT>(r);
-        *reinterpret_cast<uint4*>(yp + 8) = pack8h<DT>(r + 8);
+        *reinterpret_cast<uint4*>(yp) = make_uint4(mx[0], mx[1], mx[2], mx[3]);
+        *reinterpret_cast<uint4*>(yp + 8) = make_uint4(mx[4], mx[5], mx[6], mx[7]);
         if (a.codes != nullptr) *reinterpret_cast<uint2*>(a.codes + pp * (a.Cout >> 3) + (chb >> 3)) = make_uint2(cw0, cw1);
       }
     }
